@@ -1,0 +1,287 @@
+"""Benchmark of the DLRM embedding + interaction hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--no-cpu-baseline]
+
+One step = one training pass of the hot path over one batch (src/train/train.jl:215-227 minus
+the dense MLPs): maplookup -> DotInteraction -> dot_back -> update!(Descent) of the tables,
+with the dense vector x and dLoss/d(out) supplied as synthetic inputs already in HBM.
+Default workload (BASELINE metric): 26 Criteo-Kaggle tables (criteo.jl:350-377) x 128-dim
+fp32, 2048 samples per GPU, one-hot int32 indices drawn uniformly per table, 8 distinct
+batches cycled.  N > 1 (torchrun): tables sharded by table across ranks, per-GPU batch fixed
+(weak scaling), RCCL all-to-all of the looked-up vectors forward and of their gradients
+backward (dlrm.jl_amd/sharded.py).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import dlrm_pkg  # noqa: E402
+
+METRIC = "DLRM samples/sec (fwd+bwd), 26 tables×128-dim bs=2048; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+NBATCH = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="kaggle-d128-b2048")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    ap.add_argument("--overlap-indexer", type=int, default=1)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks):
+    """Per-launch algorithmic HBM bytes of each stage (SURVEY.md §8d formulas)."""
+    d, F = D, T + 1
+    P = F * (F - 1) // 2
+    N = B * L
+    return {
+        "lookup": T * B * (L * I + L * D * E + D * E),
+        "interact_fwd": B * (d * E + (F - 1) * D * E + d * E + (d + P) * E),
+        "interact_bwd": B * ((d + P) * E + F * D * E + F * D * 4 + d * 4),
+        "indexer_build": T * N * I + T * N * 4 + uniq * 8 + chunks * 16,
+        "sgd_update": T * N * (4 + D * 4) + uniq * 2 * D * E + chunks * 16,
+    }
+
+
+def make_inputs(pkg, w, B, dev, rank, T_rows):
+    """Tables ~ ScaledUniform (model.jl:61-65), x ~ N(0,1), dout ~ N(0, 1e-3)."""
+    g = torch.Generator(device=dev).manual_seed(51234 + rank)  # model.jl:193 seed
+    dt = torch.float32 if w["dtype"] == "f32" else torch.bfloat16
+    D, L = w["dim"], w["lookups"]
+    tables = []
+    for n in T_rows:
+        s = 1.0 / float(np.sqrt(n))
+        t = torch.empty((n, D), dtype=torch.float32, device=dev).uniform_(-s, s, generator=g)
+        tables.append(t.to(dt) if dt != torch.float32 else t)
+    idx = []
+    for _ in range(NBATCH):
+        cols = [torch.randint(0, n, (B * L,), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
+                for n in T_rows]
+        idx.append(torch.stack(cols).contiguous())
+    return tables, idx, g
+
+
+def cpu_baseline(pkg, w, seconds, threads):
+    """Times the C restatement (oracle/, OpenMP) of the same step on the host: full-size
+    tables in DRAM, same batch size.  Rank 0, N=1 only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    rows = w["rows"]
+    D, B, L = w["dim"], w["batch"], w["lookups"]
+    T = len(rows)
+    F = T + 1
+    P = F * (F - 1) // 2
+    rng = np.random.default_rng(51234)
+    tables = []
+    for t, n in enumerate(rows):
+        a = np.empty((n, D), dtype=np.float32)
+        oracle.fill_uniform(a, -1.0 / np.sqrt(n), 1.0 / np.sqrt(n), 1000 + t, threads)
+        tables.append(a)
+    batches = [np.stack([rng.integers(0, n, size=B * L) for n in rows]).astype(np.int64) for _ in range(4)]
+    x = rng.standard_normal((B, D)).astype(np.float32)
+    dout = (rng.standard_normal((B, D + P)) * 1e-3).astype(np.float32)
+    ys = np.zeros((B, F * D), dtype=np.float32)
+
+    def step(k):
+        idx = batches[k % len(batches)]
+        oracle.maplookup(tables, idx, 0, B, L, ys, D, threads)
+        oracle.interact_fwd(x, ys, F, 0, threads)
+        dx, dt = oracle.interact_bwd(dout, ys, D, F, 0, threads)
+        oracle.sgd_update(tables, idx, 0, B, L, dt, D, 0.01, threads)
+
+    step(0)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    del tables
+    return {"value": B * n / el, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"C/OpenMP restatement of the same step (oracle/dlrm_oracle.c), {T} tables x {D} "
+                      f"fp32 in host DRAM ({sum(rows) * D * 4 / 1e9:.1f} GB), B={B}, {n} timed steps "
+                      f"({el:.1f} s) after 1 warm-up; not the Julia reference (no julia toolchain)"}
+
+
+def load_pmc(workload, kernel):
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    pkg = dlrm_pkg.load()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    w = dict(pkg.WORKLOADS[a.workload])
+    B, D, L = w["batch"], w["dim"], w["lookups"]
+    rows = w["rows"]
+    T = len(rows)
+    E = 4 if w["dtype"] == "f32" else 2
+
+    if world == 1:
+        tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows)
+        ts = pkg.EmbeddingTableSet(tables)
+        engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0, overlap_indexer=bool(a.overlap_indexer))
+        F = T + 1
+        dtp = tables[0].dtype
+        x = torch.randn((B, D), device=dev, generator=g).to(dtp)
+        dout = (torch.randn((B, engine.width), device=dev, generator=g) * 1e-3).to(dtp)
+        packs = [pkg.PackedIndices(i.reshape(T, B, L)) for i in idx]
+
+        def step(k):
+            engine.step(x, packs[k % NBATCH], dout)
+    else:
+        from dlrm_jl_amd.sharded import ShardedHotPath
+        engine = ShardedHotPath(pkg, w, B, dev, rank, world, lr=a.lr)
+        step = engine.step
+
+    # warm-up (also validates indices once)
+    for k in range(max(a.warmup, 1)):
+        step(k)
+    torch.cuda.synchronize()
+    if world == 1:
+        engine.check_bounds()
+
+    graphs = None
+    if a.mode == "graph":
+        try:
+            graphs = []
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for k in range(NBATCH):
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=s):
+                        step(k)
+                    graphs.append(gr)
+            torch.cuda.current_stream().wait_stream(s)
+            for k in range(NBATCH):
+                graphs[k].replay()
+            torch.cuda.synchronize()
+        except Exception as e:  # graph capture unsupported: eager
+            print(f"note: graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
+            graphs = None
+
+    def run(k):
+        if graphs is not None:
+            graphs[k % NBATCH].replay()
+        else:
+            step(k)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        run(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ms = el * 1e3 / a.steps
+    if world > 1:
+        tt = torch.tensor([ms], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = float(tt.item())
+    value = B * world / (ms / 1e3)
+
+    # ---- per-kernel timing (HIP events on the launch stream) + roofline, rank 0
+    roofline = None
+    stages = None
+    if rank == 0 and world == 1:
+        uniq = chunks = 0
+        for k in range(NBATCH):
+            engine.build_indexer(packs[k])
+            cnt = np.zeros(8, dtype=np.int32)
+            torch.cuda.synchronize()
+            for t in range(T):
+                uniq += len(engine.indexer.unique_rows(t))
+        uniq /= NBATCH
+        chunks = uniq  # one chunk per unique row, plus a few for hot rows
+        bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks)
+        names = ["lookup", "interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(a.steps)]
+        for k in range(a.steps):
+            p = packs[k % NBATCH]
+            e = evs[k]
+            e[0].record()
+            engine.lookup(p)
+            e[1].record()
+            engine.interact_fwd(x)
+            e[2].record()
+            engine.build_indexer(p)
+            e[3].record()
+            engine.interact_bwd(dout)
+            e[4].record()
+            engine.sgd_update(p, prebuilt=True)
+            e[5].record()
+        torch.cuda.synchronize()
+        stages = {}
+        for i, n in enumerate(names):
+            us = float(np.mean([evs[k][i].elapsed_time(evs[k][i + 1]) for k in range(a.steps)])) * 1e3
+            stages[n] = {"us": round(us, 2), "alg_bytes": int(bytes_[n]),
+                         "GBps": round(bytes_[n] / (us * 1e-6) / 1e9, 1)}
+        dom = max(names, key=lambda n: stages[n]["us"])
+        ach = stages[dom]["GBps"]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(a.workload, dom),
+                    "alg_bytes_per_launch": int(bytes_[dom]), "avg_launch_us": stages[dom]["us"],
+                    "stages": stages}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and w["dtype"] == "f32":
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        try:
+            cpu = cpu_baseline(pkg, w, a.cpu_seconds, threads)
+        except Exception as e:
+            print(f"note: cpu baseline failed: {e!r}", file=sys.stderr)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": w["dtype"],
+            "data": "synthetic (uniform indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)",
+            "config": {"workload": a.workload, "tables": T, "dim": D, "batch_per_gpu": B, "global_batch": B * world,
+                       "lookups": L, "index_dtype": "int32", "table_rows": "Criteo-Kaggle (criteo.jl:350-377)",
+                       "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + all-to-all",
+                       "launch": "hipGraph replay" if graphs is not None else "eager"},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

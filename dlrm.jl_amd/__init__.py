@@ -1,0 +1,24 @@
+"""dlrm.jl_amd — MI355X-native (gfx950) DLRM embedding + feature-interaction hot path.
+
+A drop-in for the hot path of darchr/DLRM.jl: the embedding gather
+(maplookup), the pairwise-dot interaction (DotInteraction / dot_back) and the sparse SGD
+update (update!), as hand-written HIP kernels behind the C ABI in include/dlrm_hip.h.
+Import name: `dlrm_jl_amd` (the directory name carries a dot; see dlrm_pkg.py).
+"""
+from . import _lib
+from ._lib import BoundsError, DLRMError, LibraryMissing
+from .embedding import (DefaultStrategy, EmbeddingTableSet, PackedIndices, PreallocationStrategy, SimpleEmbedding,
+                        lookup, maplookup)
+from .hotpath import HotPath
+from .interact import (POST_INTERACTION_PAD_TO_MUL, DotInteraction, cdiv, dot_back, fast_vcat, interaction_sizes,
+                       rrule, up_to_mul_of)
+from .shapes import KAGGLE_EMBEDDING_SIZES, TERABYTE_EMBEDDING_SIZES, WORKLOADS
+from .update import Descent, SparseEmbeddingUpdate, SparseIndexer, maplookup_pullback, update_
+
+__all__ = [
+    "BoundsError", "DLRMError", "LibraryMissing", "DefaultStrategy", "EmbeddingTableSet", "PackedIndices",
+    "PreallocationStrategy", "SimpleEmbedding", "lookup", "maplookup", "HotPath", "POST_INTERACTION_PAD_TO_MUL",
+    "DotInteraction", "cdiv", "dot_back", "fast_vcat", "interaction_sizes", "rrule", "up_to_mul_of",
+    "KAGGLE_EMBEDDING_SIZES", "TERABYTE_EMBEDDING_SIZES", "WORKLOADS", "Descent", "SparseEmbeddingUpdate",
+    "SparseIndexer", "maplookup_pullback", "update_",
+]

@@ -1,0 +1,402 @@
+// abi.cpp — the extern "C" boundary declared in include/dlrm_hip.h.
+//
+// Owns the three handle types (ctx, tables, indexer), validates arguments on the host,
+// maps HIP errors to dlrm_status codes and forwards to the kernel launchers.  No launching
+// entry point allocates or synchronises (hipGraph-capturable); the one exception is the
+// first dlrm_sgd_update on an indexer, which sizes its partial-sum scratch once.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "common.hpp"
+
+using namespace dlrm;
+
+struct dlrm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    unsigned* err = nullptr;  // device error word
+    int cus = 256;
+    char msg[512] = {0};
+};
+
+struct dlrm_tables {
+    dlrm_ctx* ctx = nullptr;
+    int T = 0, D = 0, dtype = 0;
+    TableDesc* d_desc = nullptr;
+    std::vector<TableDesc> h_desc;
+    bool aligned16 = true;
+};
+
+struct dlrm_indexer {
+    dlrm_ctx* ctx = nullptr;
+    int T = 0;
+    IndexerDev dev{};
+    void* block = nullptr;  // one allocation for every array
+    float* partial = nullptr;
+    size_t partial_bytes = 0;
+    // recorded by the last build
+    bool built = false;
+    const void* indices = nullptr;
+    int itype = 0, base = 0, B = 0, L = 0;
+    int64_t tstride = 0;
+};
+
+namespace dlrm {
+unsigned* ctx_error_word(dlrm_ctx* ctx) { return ctx->err; }
+hipStream_t ctx_stream(dlrm_ctx* ctx) { return ctx->stream; }
+int ctx_num_cus(dlrm_ctx* ctx) { return ctx->cus; }
+int ctx_fail(dlrm_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(ctx->msg, sizeof(ctx->msg), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what) {
+    if (e == hipSuccess) return DLRM_OK;
+    return ctx_fail(ctx, e == hipErrorOutOfMemory ? DLRM_E_NOMEM : DLRM_E_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+}  // namespace dlrm
+
+#define CHECK_ARG(cond, ...) \
+    do {                     \
+        if (!(cond)) return ctx_fail(ctx, DLRM_E_ARG, __VA_ARGS__); \
+    } while (0)
+
+static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice"); }
+
+extern "C" {
+
+int dlrm_abi_version(void) { return DLRM_HIP_ABI_VERSION; }
+
+int dlrm_ctx_create(int device, void* stream, dlrm_ctx** out) {
+    if (!out) return DLRM_E_ARG;
+    *out = nullptr;
+    dlrm_ctx* ctx = new (std::nothrow) dlrm_ctx();
+    if (!ctx) return DLRM_E_NOMEM;
+    ctx->device = device;
+    ctx->stream = (hipStream_t)stream;
+    int rc = hip_set(ctx);
+    if (rc == DLRM_OK) {
+        hipDeviceProp_t prop;
+        rc = ctx_hip(ctx, hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+        if (rc == DLRM_OK) ctx->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    }
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMalloc((void**)&ctx->err, 16), "hipMalloc(err)");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemset(ctx->err, 0, 16), "hipMemset(err)");
+    if (rc != DLRM_OK) {
+        if (ctx->err) (void)hipFree(ctx->err);
+        delete ctx;
+        return rc;
+    }
+    *out = ctx;
+    return DLRM_OK;
+}
+
+int dlrm_ctx_destroy(dlrm_ctx* ctx) {
+    if (!ctx) return DLRM_OK;
+    if (ctx->err) (void)hipFree(ctx->err);
+    delete ctx;
+    return DLRM_OK;
+}
+
+int dlrm_ctx_set_stream(dlrm_ctx* ctx, void* stream) {
+    if (!ctx) return DLRM_E_ARG;
+    ctx->stream = (hipStream_t)stream;
+    return DLRM_OK;
+}
+
+const char* dlrm_last_error(const dlrm_ctx* ctx) { return ctx ? ctx->msg : "null context"; }
+
+int dlrm_sync(dlrm_ctx* ctx) {
+    if (!ctx) return DLRM_E_ARG;
+    return ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+int dlrm_check_bounds(dlrm_ctx* ctx) {
+    if (!ctx) return DLRM_E_ARG;
+    unsigned h = 0;
+    int rc = ctx_hip(ctx, hipMemcpyAsync(&h, ctx->err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream),
+                     "read error word");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemsetAsync(ctx->err, 0, sizeof(unsigned), ctx->stream), "clear error word");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (rc != DLRM_OK) return rc;
+    if (h & kErrIndex) return ctx_fail(ctx, DLRM_E_INDEX, "BoundsError: an embedding index was out of range");
+    return DLRM_OK;
+}
+
+int dlrm_malloc(dlrm_ctx* ctx, size_t bytes, void** dptr) {
+    CHECK_ARG(ctx && dptr, "dlrm_malloc: null argument");
+    *dptr = nullptr;
+    if (bytes == 0) return DLRM_OK;
+    return ctx_hip(ctx, hipMalloc(dptr, bytes), "hipMalloc");
+}
+
+int dlrm_free(dlrm_ctx* ctx, void* dptr) {
+    CHECK_ARG(ctx, "dlrm_free: null ctx");
+    if (!dptr) return DLRM_OK;
+    return ctx_hip(ctx, hipFree(dptr), "hipFree");
+}
+
+int dlrm_memcpy_h2d(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    CHECK_ARG(ctx && (bytes == 0 || (dst && src)), "dlrm_memcpy_h2d: null argument");
+    int rc = ctx_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream), "memcpy h2d");
+    return rc ? rc : ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+int dlrm_memcpy_d2h(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    CHECK_ARG(ctx && (bytes == 0 || (dst && src)), "dlrm_memcpy_d2h: null argument");
+    int rc = ctx_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream), "memcpy d2h");
+    return rc ? rc : ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+// ---------------------------------------------------------------------------- tables
+int dlrm_tables_create(dlrm_ctx* ctx, int num_tables, int dim, int dtype, void* const* data, const int64_t* nrows,
+                       dlrm_tables** out) {
+    CHECK_ARG(ctx && out, "dlrm_tables_create: null argument");
+    *out = nullptr;
+    CHECK_ARG(num_tables >= 0 && dim > 0, "dlrm_tables_create: num_tables=%d dim=%d", num_tables, dim);
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_tables_create: unknown dtype %d", dtype);
+    CHECK_ARG(num_tables == 0 || (data && nrows), "dlrm_tables_create: null data/nrows");
+    dlrm_tables* tb = new (std::nothrow) dlrm_tables();
+    if (!tb) return DLRM_E_NOMEM;
+    tb->ctx = ctx;
+    tb->T = num_tables;
+    tb->D = dim;
+    tb->dtype = dtype;
+    tb->h_desc.resize(num_tables);
+    for (int t = 0; t < num_tables; ++t) {
+        if (nrows[t] < 0 || nrows[t] >= 0xFFFFFFFFll || (nrows[t] > 0 && !data[t])) {
+            delete tb;
+            return ctx_fail(ctx, DLRM_E_ARG, "dlrm_tables_create: table %d has nrows=%lld", t, (long long)nrows[t]);
+        }
+        tb->h_desc[t].data = data[t];
+        tb->h_desc[t].nrows = nrows[t];
+        if ((uintptr_t)data[t] % 16) tb->aligned16 = false;
+    }
+    int rc = hip_set(ctx);
+    if (rc == DLRM_OK && num_tables > 0) {
+        rc = ctx_hip(ctx, hipMalloc((void**)&tb->d_desc, sizeof(TableDesc) * num_tables), "hipMalloc(tables)");
+        if (rc == DLRM_OK)
+            rc = ctx_hip(ctx, hipMemcpy(tb->d_desc, tb->h_desc.data(), sizeof(TableDesc) * num_tables,
+                                        hipMemcpyHostToDevice), "hipMemcpy(tables)");
+    }
+    if (rc != DLRM_OK) {
+        if (tb->d_desc) (void)hipFree(tb->d_desc);
+        delete tb;
+        return rc;
+    }
+    *out = tb;
+    return DLRM_OK;
+}
+
+int dlrm_tables_destroy(dlrm_tables* tb) {
+    if (!tb) return DLRM_OK;
+    if (tb->d_desc) (void)hipFree(tb->d_desc);
+    delete tb;
+    return DLRM_OK;
+}
+
+static int check_indices(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype, int64_t tstride,
+                         int batch, int lookups) {
+    CHECK_ARG(itype == DLRM_I32 || itype == DLRM_I64, "unknown index type %d", itype);
+    CHECK_ARG(batch >= 0 && lookups >= 1, "batch=%d lookups=%d", batch, lookups);
+    CHECK_ARG((int64_t)batch * lookups < (1ll << 31), "batch*lookups exceeds 2^31");
+    CHECK_ARG(batch == 0 || tb->T == 0 || indices, "null indices");
+    CHECK_ARG(tb->T <= 1 || tstride >= (int64_t)batch * lookups, "table_stride %lld < batch*lookups %lld",
+              (long long)tstride, (long long)batch * lookups);
+    return DLRM_OK;
+}
+
+int dlrm_maplookup(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype, int64_t table_stride,
+                   int index_base, int batch, int lookups, void* out, int64_t out_ld, int64_t out_offset) {
+    CHECK_ARG(ctx && tb, "dlrm_maplookup: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    CHECK_ARG(batch == 0 || tb->T == 0 || out, "dlrm_maplookup: null out");
+    CHECK_ARG(out_offset >= 0 && out_ld >= out_offset + (int64_t)tb->T * tb->D,
+              "dlrm_maplookup: out_ld %lld < out_offset %lld + T*D %lld", (long long)out_ld, (long long)out_offset,
+              (long long)tb->T * tb->D);
+    return launch_maplookup(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype, table_stride,
+                            index_base, batch, lookups, out, out_ld, out_offset);
+}
+
+// ---------------------------------------------------------------------- interaction
+int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* x, int64_t x_ld,
+                      void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {
+    CHECK_ARG(ctx, "dlrm_interact_fwd: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_interact_fwd: dtype %d", dtype);
+    CHECK_ARG(d > 0 && num_features >= 1 && batch >= 0 && padding >= 0, "dlrm_interact_fwd: d=%d F=%d B=%d pad=%d", d,
+              num_features, batch, padding);
+    const int64_t P = (int64_t)num_features * (num_features - 1) / 2;
+    CHECK_ARG(x_ld >= d && ys_ld >= (int64_t)num_features * d && out_ld >= d + P + padding,
+              "dlrm_interact_fwd: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (x && ys && out), "dlrm_interact_fwd: null buffer");
+    return launch_interact_fwd(ctx, dtype, d, num_features, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
+}
+
+int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* dout, int64_t dout_ld,
+                      int padding, const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
+    CHECK_ARG(ctx, "dlrm_interact_bwd: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_interact_bwd: dtype %d", dtype);
+    CHECK_ARG(d > 0 && num_features >= 1 && batch >= 0 && padding >= 0, "dlrm_interact_bwd: d=%d F=%d B=%d", d,
+              num_features, batch);
+    const int64_t P = (int64_t)num_features * (num_features - 1) / 2;
+    CHECK_ARG(dout_ld >= d + P + padding && t_ld >= (int64_t)num_features * d && dx_ld >= d &&
+                  dt_ld >= (int64_t)num_features * d,
+              "dlrm_interact_bwd: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (dout && t && dx && dt), "dlrm_interact_bwd: null buffer");
+    return launch_interact_bwd(ctx, dtype, d, num_features, batch, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
+}
+
+// --------------------------------------------------------------------------- indexer
+int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm_indexer** out) {
+    CHECK_ARG(ctx && out, "dlrm_indexer_create: null argument");
+    *out = nullptr;
+    CHECK_ARG(num_tables >= 0 && max_lookups >= 0 && max_lookups < (1ll << 31), "dlrm_indexer_create: T=%d cap=%lld",
+              num_tables, (long long)max_lookups);
+    dlrm_indexer* ix = new (std::nothrow) dlrm_indexer();
+    if (!ix) return DLRM_E_NOMEM;
+    ix->ctx = ctx;
+    ix->T = num_tables;
+    const int64_t cap = max_lookups > 0 ? max_lookups : 1;
+    const int64_t T = num_tables > 0 ? num_tables : 1;
+    ix->dev.cap = cap;
+    ix->dev.hot_cap = cap / 16 + 2;  // sum over hot segments of ceil(len/32) <= 2*N/32
+    // carve every array out of one allocation (16-B aligned pieces)
+    struct Piece { void** p; size_t bytes; };
+    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1));
+    Piece pieces[] = {
+        {(void**)&ix->dev.keys0, n * 4},     {(void**)&ix->dev.keys1, n * 4},   {(void**)&ix->dev.vals0, n * 4},
+        {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
+        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.ch_beg, n * 4},  {(void**)&ix->dev.ch_end, n * 4},
+        {(void**)&ix->dev.ch_row, n * 4},    {(void**)&ix->dev.ch_slot, n * 4}, {(void**)&ix->dev.hot_row, n * 4},
+        {(void**)&ix->dev.hot_slot0, n * 4}, {(void**)&ix->dev.hot_n, n * 4},  {(void**)&ix->dev.counts, (size_t)T * 32},
+    };
+    size_t total = 0;
+    for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
+    int rc = hip_set(ctx);
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMalloc(&ix->block, total), "hipMalloc(indexer)");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemset(ix->block, 0, total), "hipMemset(indexer)");
+    if (rc != DLRM_OK) {
+        if (ix->block) (void)hipFree(ix->block);
+        delete ix;
+        return rc;
+    }
+    char* base = (char*)ix->block;
+    for (auto& pc : pieces) {
+        *pc.p = base;
+        base += (pc.bytes + 255) & ~(size_t)255;
+    }
+    *out = ix;
+    return DLRM_OK;
+}
+
+int dlrm_indexer_destroy(dlrm_indexer* ix) {
+    if (!ix) return DLRM_OK;
+    if (ix->block) (void)hipFree(ix->block);
+    if (ix->partial) (void)hipFree(ix->partial);
+    delete ix;
+    return DLRM_OK;
+}
+
+int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, const void* indices, int itype,
+                       int64_t table_stride, int index_base, int batch, int lookups) {
+    CHECK_ARG(ctx && ix && tb, "dlrm_indexer_build: null argument");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    CHECK_ARG(tb->T == ix->T, "dlrm_indexer_build: indexer has %d tables, tables has %d", ix->T, tb->T);
+    CHECK_ARG((int64_t)batch * lookups <= ix->dev.cap, "dlrm_indexer_build: batch*lookups %lld > capacity %lld",
+              (long long)batch * lookups, (long long)ix->dev.cap);
+    rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups);
+    if (rc) return rc;
+    ix->built = true;
+    ix->indices = indices;
+    ix->itype = itype;
+    ix->tstride = table_stride;
+    ix->base = index_base;
+    ix->B = batch;
+    ix->L = lookups;
+    return DLRM_OK;
+}
+
+int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t* num_unique, int64_t* rows,
+                      int64_t* positions, int64_t* seg_start, int64_t cap) {
+    CHECK_ARG(ctx && ix && num_unique, "dlrm_indexer_read: null argument");
+    CHECK_ARG(ix->built, "dlrm_indexer_read: indexer not built");
+    CHECK_ARG(table >= 0 && table < ix->T, "dlrm_indexer_read: table %d", table);
+    int rc = ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (rc) return rc;
+    int32_t cnt[8];
+    rc = ctx_hip(ctx, hipMemcpy(cnt, ix->dev.counts + (int64_t)table * 8, sizeof(cnt), hipMemcpyDeviceToHost), "read");
+    if (rc) return rc;
+    *num_unique = cnt[0];
+    const int64_t U = cnt[0], NV = cnt[4];
+    const int64_t off = (int64_t)table * ix->dev.cap;
+    if (rows) {
+        const int64_t n = U < cap ? U : cap;
+        std::vector<uint32_t> tmp(n > 0 ? n : 1);
+        if (n) rc = ctx_hip(ctx, hipMemcpy(tmp.data(), ix->dev.seg_row + off, n * 4, hipMemcpyDeviceToHost), "read");
+        for (int64_t i = 0; i < n; ++i) rows[i] = tmp[i];
+    }
+    if (positions && seg_start && rc == DLRM_OK) {
+        const int64_t n = NV < cap ? NV : cap;
+        std::vector<int32_t> tmp((n > 0 ? n : 1));
+        if (n) rc = ctx_hip(ctx, hipMemcpy(tmp.data(), ix->dev.perm + off, n * 4, hipMemcpyDeviceToHost), "read");
+        for (int64_t i = 0; i < n; ++i) positions[i] = tmp[i];
+        const int64_t ns = (U + 1) < (cap + 1) ? (U + 1) : (cap + 1);
+        std::vector<int32_t> tmp2(ns);
+        if (rc == DLRM_OK)
+            rc = ctx_hip(ctx, hipMemcpy(tmp2.data(), ix->dev.seg_start + (int64_t)table * (ix->dev.cap + 1), ns * 4,
+                                        hipMemcpyDeviceToHost), "read");
+        for (int64_t i = 0; i < ns; ++i) seg_start[i] = tmp2[i];
+    }
+    return rc;
+}
+
+int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned flags, const void* indices, int itype,
+                    int64_t table_stride, int index_base, int batch, int lookups, const void* grad, int grad_dtype,
+                    int64_t grad_ld, int64_t grad_offset, float lr) {
+    CHECK_ARG(ctx && tb, "dlrm_sgd_update: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    CHECK_ARG(grad_dtype == DLRM_F32 || grad_dtype == DLRM_BF16, "dlrm_sgd_update: grad dtype %d", grad_dtype);
+    CHECK_ARG(grad_offset >= 0 && grad_ld >= grad_offset + (int64_t)tb->T * tb->D, "dlrm_sgd_update: grad_ld too small");
+    CHECK_ARG(batch == 0 || tb->T == 0 || grad, "dlrm_sgd_update: null grad");
+    if (flags & DLRM_UPDATE_ATOMIC) {
+        if (tb->dtype != DLRM_F32)
+            return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_sgd_update: atomic mode needs fp32 tables");
+        return launch_sgd_atomic(ctx, tb->d_desc, tb->T, tb->D, indices, itype, table_stride, index_base, batch,
+                                 lookups, grad, grad_dtype, grad_ld, grad_offset, lr);
+    }
+    CHECK_ARG(ix, "dlrm_sgd_update: deterministic mode needs an indexer");
+    if (flags & DLRM_UPDATE_PREBUILT) {
+        if (!ix->built || ix->indices != indices || ix->B != batch || ix->L != lookups || ix->itype != itype ||
+            ix->tstride != table_stride || ix->base != index_base)
+            return ctx_fail(ctx, DLRM_E_STATE, "dlrm_sgd_update: indexer was not built from these indices");
+    } else {
+        rc = dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, lookups);
+        if (rc) return rc;
+    }
+    const size_t need = sizeof(float) * (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.hot_cap * (size_t)tb->D;
+    if (ix->partial_bytes < need) {  // sized once per (indexer, dim)
+        if (ix->partial) (void)hipFree(ix->partial);
+        ix->partial = nullptr;
+        ix->partial_bytes = 0;
+        rc = ctx_hip(ctx, hipMalloc((void**)&ix->partial, need), "hipMalloc(partial)");
+        if (rc) return rc;
+        ix->partial_bytes = need;
+    }
+    return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
+                            (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr, ix->partial);
+}
+
+}  // extern "C"

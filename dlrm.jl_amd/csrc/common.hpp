@@ -1,0 +1,114 @@
+// common.hpp — shared device helpers for the gfx950 DLRM hot-path kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dlrm_hip.h"
+
+namespace dlrm {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// Device-side descriptor of one embedding table (SimpleEmbedding{Static{D}}.data).
+struct TableDesc {
+    void* data;     // [nrows][dim] row-major, f32 or bf16
+    int64_t nrows;
+};
+
+// Device-side error word: bit 0 = an out-of-range index was skipped.
+constexpr unsigned kErrIndex = 1u;
+
+__device__ __forceinline__ void raise_index_error(unsigned* err) {
+    __hip_atomic_fetch_or(err, kErrIndex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even; NaN stays NaN (MI355X_MICROARCH.md, correctness boundaries).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (uint16_t)((u >> 16) | 0x40);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ int64_t load_index(const void* idx, int itype, int64_t i) {
+    return itype == DLRM_I64 ? ((const int64_t*)idx)[i] : (int64_t)((const int32_t*)idx)[i];
+}
+
+// 16-byte vector types
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+// Element traits: storage type -> 16-byte vector of it, element count per vector.
+template <typename T> struct Vec;
+template <> struct Vec<float> {
+    static constexpr int N = 4;
+    typedef f32x4 type;
+    __device__ static inline void to_f32(const type& v, float* o) { o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3]; }
+    __device__ static inline type from_f32(const float* o) { type v; v[0] = o[0]; v[1] = o[1]; v[2] = o[2]; v[3] = o[3]; return v; }
+};
+template <> struct Vec<uint16_t> {
+    static constexpr int N = 8;
+    typedef u16x8 type;
+    __device__ static inline void to_f32(const type& v, float* o) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = bf16_to_f32(v[i]);
+    }
+    __device__ static inline type from_f32(const float* o) {
+        type v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = f32_to_bf16(o[i]);
+        return v;
+    }
+};
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(uint16_t v) { return bf16_to_f32(v); }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ uint16_t from_f32<uint16_t>(float v) { return f32_to_bf16(v); }
+
+}  // namespace dlrm
+
+namespace dlrm {
+// Per-table indexer arrays (device), each [T][cap] (seg_start [T][cap+1]).
+struct IndexerDev {
+    uint32_t* keys0;  uint32_t* keys1;   // global sort scratch (cap > kLdsSortMax)
+    int32_t* vals0;   int32_t* vals1;
+    int32_t* perm;         // sorted positions (valid prefix)
+    int32_t* seg_start;    // [cap+1]
+    uint32_t* seg_row;
+    int32_t* ch_beg;  int32_t* ch_end;  uint32_t* ch_row;  int32_t* ch_slot;
+    uint32_t* hot_row; int32_t* hot_slot0; int32_t* hot_n;
+    int32_t* counts;       // [T][8]: U, chunks, hot, hot_chunks, nvalid
+    int64_t cap;
+    int64_t hot_cap;       // hot-chunk slots per table
+};
+
+}  // namespace dlrm
+
+// Host-side launch helpers (defined in abi.cpp) and the per-kernel launchers.
+struct dlrm_ctx;
+namespace dlrm {
+unsigned* ctx_error_word(dlrm_ctx* ctx);
+hipStream_t ctx_stream(dlrm_ctx* ctx);
+int ctx_fail(dlrm_ctx* ctx, int code, const char* fmt, ...);
+int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what);
+int ctx_num_cus(dlrm_ctx* ctx);
+
+int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
+                     const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
+                     int64_t out_ld, int64_t out_off);
+int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
+                        int64_t ys_ld, void* out, int64_t out_ld, int padding);
+int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
+                        const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
+int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
+                         int itype, int64_t tstride, int base, int B, int L);
+int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
+                     int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
+                     float lr, float* partial);
+int launch_sgd_atomic(dlrm_ctx* ctx, TableDesc* tabs, int T, int D, const void* idx, int itype, int64_t tstride,
+                      int base, int B, int L, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
+                      float lr);
+}  // namespace dlrm

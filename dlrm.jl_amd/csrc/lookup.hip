@@ -1,0 +1,179 @@
+// lookup.hip — maplookup(PreallocationStrategy(P), tables, sparse) on gfx950.
+//
+// Reference: EmbeddingTables.maplookup (un-vendored), called at src/model/model.jl:161;
+// semantics pinned by test/model/embedding_update.jl:23-33 and the golden
+// `concatenated_result` of ref/pytorch_reference_{single,multi}.hdf5.
+//
+//   out[b][P + t*D + c] = sum_{k<L} table_t[idx_t[b*L + k] - base][c]
+//
+// HBM-bound row gather.  Each output row (one (sample, table) pair) is D*E bytes; a wave
+// splits into RPW row groups of LPR lanes, each lane moving 16 B per access, so every
+// wave-instruction reads RPW whole rows (coalesced 16-B lanes) and writes them back as one
+// contiguous run (items are ordered b-major so consecutive tables of a sample are adjacent
+// in the output).  Every lane keeps U independent row loads in flight before it stores.
+// Pooled bags (L > 1) are seeded with the first row and accumulated in k order in fp32
+// (an exact copy for L = 1), then rounded once to the table dtype.
+#include "common.hpp"
+
+namespace dlrm {
+
+template <typename T, int VPR, int U>
+__global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict__ tabs, int ntab,
+                                                     const void* __restrict__ idx, int itype,
+                                                     int64_t tstride, int base, int B, int L,
+                                                     T* __restrict__ out, int64_t out_ld, int64_t out_off,
+                                                     unsigned* __restrict__ err) {
+    typedef Vec<T> V;
+    constexpr int NE = V::N;                       // elements per 16-B vector
+    constexpr int LPR = VPR <= 64 ? VPR : 64;      // lanes per row
+    constexpr int VPL = VPR <= 64 ? 1 : VPR / 64;  // vectors per lane
+    constexpr int RPW = 64 / LPR;                  // rows per wave-instruction
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR, v = lane % LPR;
+    if (g >= RPW) return;  // idle lanes when LPR does not divide 64
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t total = (int64_t)ntab * B;
+    constexpr int D = VPR * NE;
+
+    for (int64_t first = wave * (RPW * U); first < total; first += nwaves * (RPW * U)) {
+        int64_t item[U];
+        const T* rowp[U];
+        bool live[U];
+        float acc[U][VPL][NE];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            item[u] = first + u * RPW + g;
+            live[u] = item[u] < total;
+        }
+        for (int k = 0; k < L; ++k) {
+            typename V::type vv[U][VPL];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                rowp[u] = nullptr;
+                if (live[u]) {
+                    const int64_t b = item[u] / ntab;
+                    const int t = (int)(item[u] - b * ntab);
+                    const int64_t r = load_index(idx, itype, t * tstride + b * L + k) - base;
+                    if (r >= 0 && r < tabs[t].nrows) rowp[u] = (const T*)tabs[t].data + r * D;
+                    else if (v == 0) raise_index_error(err);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) {
+                    if (rowp[u]) vv[u][j] = *((const typename V::type*)(rowp[u]) + v + j * 64);
+                    else vv[u][j] = typename V::type{};
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) {
+                    float f[NE];
+                    V::to_f32(vv[u][j], f);
+#pragma unroll
+                    for (int e = 0; e < NE; ++e) acc[u][j][e] = (k == 0) ? f[e] : acc[u][j][e] + f[e];
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            const int64_t b = item[u] / ntab;
+            const int t = (int)(item[u] - b * ntab);
+            T* o = out + b * out_ld + out_off + (int64_t)t * D;
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) *((typename V::type*)o + v + j * 64) = V::from_f32(acc[u][j]);
+        }
+    }
+}
+
+// Scalar fallback for shapes / alignments the vector kernel does not take.
+template <typename T>
+__global__ __launch_bounds__(256) void maplookup_scalar(const TableDesc* __restrict__ tabs, int ntab, int D,
+                                                        const void* __restrict__ idx, int itype,
+                                                        int64_t tstride, int base, int B, int L,
+                                                        T* __restrict__ out, int64_t out_ld, int64_t out_off,
+                                                        unsigned* __restrict__ err) {
+    const int64_t total = (int64_t)ntab * B * D;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % D);
+        const int64_t item = e / D;
+        const int64_t b = item / ntab;
+        const int t = (int)(item - b * ntab);
+        float acc = 0.0f;
+        for (int k = 0; k < L; ++k) {
+            const int64_t r = load_index(idx, itype, t * tstride + b * L + k) - base;
+            float f = 0.0f;
+            if (r >= 0 && r < tabs[t].nrows) f = to_f32(((const T*)tabs[t].data)[r * D + c]);
+            else if (c == 0) raise_index_error(err);
+            acc = (k == 0) ? f : acc + f;
+        }
+        out[b * out_ld + out_off + (int64_t)t * D + c] = from_f32<T>(acc);
+    }
+}
+
+template <typename T, int VPR>
+static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx, int itype,
+                       int64_t tstride, int base, int B, int L, void* out, int64_t out_ld, int64_t out_off,
+                       unsigned* err) {
+    constexpr int LPR = VPR <= 64 ? VPR : 64;
+    constexpr int RPW = 64 / LPR;
+    constexpr int U = 4;
+    const int64_t total = (int64_t)T_ * B;
+    const int64_t waves = (total + RPW * U - 1) / (RPW * U);
+    int64_t blocks = (waves + 3) / 4;
+    const int64_t cap = (int64_t)cus * 16;  // grid-stride beyond 16 blocks per CU
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((maplookup_vec<T, VPR, U>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx, itype,
+                       tstride, base, B, L, (T*)out, out_ld, out_off, err);
+}
+
+template <typename T>
+static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx,
+                         int itype, int64_t tstride, int base, int B, int L, void* out, int64_t out_ld,
+                         int64_t out_off, unsigned* err) {
+#define DLRM_CASE(N) \
+    case N: launch_vec<T, N>(s, cus, tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err); return true;
+    switch (vpr) {
+        DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64)
+        DLRM_CASE(128) DLRM_CASE(256)
+        default: return false;
+    }
+#undef DLRM_CASE
+}
+
+int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T_, int D, int dtype,
+                     const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
+                     int64_t out_ld, int64_t out_off) {
+    if (T_ == 0 || B == 0) return DLRM_OK;
+    hipStream_t s = ctx_stream(ctx);
+    unsigned* err = ctx_error_word(ctx);
+    const int cus = ctx_num_cus(ctx);
+    const int esz = dtype == DLRM_F32 ? 4 : 2;
+    const bool aligned = tabs_aligned16 && ((uintptr_t)out % 16 == 0) && ((out_ld * esz) % 16 == 0) &&
+                         ((out_off * esz) % 16 == 0) && ((D * esz) % 16 == 0);
+    bool done = false;
+    if (aligned) {
+        const int vpr = D * esz / 16;
+        done = dtype == DLRM_F32
+                   ? dispatch_vec<float>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err)
+                   : dispatch_vec<uint16_t>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err);
+    }
+    if (!done) {
+        const int64_t total = (int64_t)T_ * B * D;
+        int64_t blocks = (total + 255) / 256;
+        if (blocks > (int64_t)cus * 16) blocks = (int64_t)cus * 16;
+        if (dtype == DLRM_F32)
+            hipLaunchKernelGGL(maplookup_scalar<float>, dim3((unsigned)blocks), dim3(256), 0, s, d_tabs, T_, D, idx,
+                               itype, tstride, base, B, L, (float*)out, out_ld, out_off, err);
+        else
+            hipLaunchKernelGGL(maplookup_scalar<uint16_t>, dim3((unsigned)blocks), dim3(256), 0, s, d_tabs, T_, D, idx,
+                               itype, tstride, base, B, L, (uint16_t*)out, out_ld, out_off, err);
+    }
+    return ctx_hip(ctx, hipGetLastError(), "maplookup launch");
+}
+
+}  // namespace dlrm

@@ -1,0 +1,549 @@
+// update.hip — SparseIndexer + EmbeddingTables.update!(Descent(lr), ...) on gfx950.
+//
+// Reference: src/train/train.jl:274-292 (SparseIndexer per table, update! with num_splits /
+// nthreads), checked by src/validation.jl:125-146 against the PyTorch `update_emb_*`.
+//
+//   table_t[r] -= lr * sum_{(b,k): idx_t[b*L+k] - base == r} grad[b][offset + t*D : +D]
+//
+// Deterministic design (the default):
+//  1. indexer_build (one 1024-thread workgroup per table): stable LSD radix sort of the
+//     table's B*L lookup positions by row (8-bit digits, only ceil(log2(nrows+1)) key bits,
+//     so a 3-row table sorts in one 2-bit pass), keys/values kept in LDS when they fit.
+//     Wave-level ranking uses 64-lane ballots (multi-split), cross-wave offsets go through
+//     LDS, so equal rows keep ascending positions.  Then, still in the workgroup: unique
+//     segments (one per touched row), and a CHUNK work list — segments longer than kChunk
+//     positions (hot rows of small tables: a 3-row table gets ~680 hits per row at B=2048)
+//     are split so that no wave serialises on a hot row.
+//  2. sgd_chunks (grid over all chunks): one lane group per chunk streams its grad rows in
+//     ascending position order (fp32 sum, 16-B lanes, 4 rows in flight), then either
+//     read-modify-writes the table row once (single-chunk segment) or stores a partial sum.
+//  3. sgd_hot: hot segments add their partials in chunk order and write the row once.
+// Every touched row is written exactly once, with a summation order fixed by positions:
+// bitwise reproducible.  DLRM_UPDATE_ATOMIC instead adds -lr*g straight into the table
+// with global_atomic_add_f32 (no sort, non-deterministic rounding order).
+#include "common.hpp"
+
+namespace dlrm {
+
+constexpr int kBuildThreads = 1024;
+constexpr int kBuildWaves = kBuildThreads / 64;
+constexpr int kChunk = 32;          // positions per chunk
+constexpr int kLdsSortMax = 2048;   // positions per table sorted entirely in LDS
+
+enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_HC = 3, CNT_NV = 4 };
+
+// Exclusive scan over the 1024 threads of the block; returns this thread's prefix, total in *tot.
+__device__ __forceinline__ int block_scan_excl(int v, int* wtot, int* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int t = lane < kBuildWaves ? wtot[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(t, off, 64);
+            if (lane >= off) t += y;
+        }
+        if (lane < kBuildWaves) wtot[kBuildWaves + lane] = t;  // inclusive wave totals
+    }
+    __syncthreads();
+    const int before = w ? wtot[kBuildWaves + w - 1] : 0;
+    *tot = wtot[2 * kBuildWaves - 1];
+    __syncthreads();  // wtot reusable after return
+    return before + x - v;
+}
+
+struct SortLds {
+    int hist[kBuildWaves][256];
+    int cnt[kBuildWaves][256];
+    int digit_off[256];
+    int wtot[2 * kBuildWaves];
+    int nvalid;
+};
+
+template <bool IN_LDS>
+__global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
+    IndexerDev ix, const TableDesc* __restrict__ tabs, const void* __restrict__ idx, int itype,
+    int64_t tstride, int base, int B, int L, unsigned* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    __shared__ SortLds sl;
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int N = B * L;
+    const int64_t off = (int64_t)t * ix.cap;
+    const uint32_t nrows = (uint32_t)tabs[t].nrows;  // host checks nrows < 2^32 - 1
+    const uint32_t sentinel = nrows;
+    const int nbits = 32 - __clz(nrows);             // bits of the sentinel value
+    const int passes = nbits == 0 ? 1 : (nbits + 7) / 8;
+
+    uint32_t* kbuf[2];
+    int32_t* vbuf[2];
+    if (IN_LDS) {
+        kbuf[0] = (uint32_t*)dyn;
+        kbuf[1] = kbuf[0] + kLdsSortMax;
+        vbuf[0] = (int32_t*)(kbuf[1] + kLdsSortMax);
+        vbuf[1] = vbuf[0] + kLdsSortMax;
+    } else {
+        kbuf[0] = ix.keys0 + off; kbuf[1] = ix.keys1 + off;
+        vbuf[0] = ix.vals0 + off; vbuf[1] = ix.vals1 + off;
+    }
+    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+
+    for (int pass = 0; pass < passes; ++pass) {
+        const int shift = 8 * pass;
+        const int dbits = nbits - shift < 8 ? (nbits - shift > 0 ? nbits - shift : 0) : 8;
+        const uint32_t mask = (1u << dbits) - 1u;
+        const uint32_t* kin = kbuf[pass & 1];
+        const int32_t* vin = vbuf[pass & 1];
+        uint32_t* kout = kbuf[(pass + 1) & 1];
+        int32_t* vout = vbuf[(pass + 1) & 1];
+
+        for (int e = tid; e < kBuildWaves * 256; e += kBuildThreads) (&sl.hist[0][0])[e] = 0;
+        __syncthreads();
+        // histogram; pass 0 reads the raw indices and validates them
+        for (int i = tid; i < N; i += kBuildThreads) {
+            uint32_t key;
+            if (pass == 0) {
+                const int64_t r = load_index(idx, itype, t * tstride + i) - base;
+                if (r >= 0 && r < (int64_t)nrows) key = (uint32_t)r;
+                else { key = sentinel; raise_index_error(err); }
+            } else {
+                key = kin[i];
+            }
+            atomicAdd(&sl.hist[w][(key >> shift) & mask], 1);
+        }
+        __syncthreads();
+        {
+            int tot = 0;
+            int v = 0;
+            if (tid < 256) for (int ww = 0; ww < kBuildWaves; ++ww) v += sl.hist[ww][tid];
+            const int ex = block_scan_excl(tid < 256 ? v : 0, sl.wtot, &tot);
+            if (tid < 256) sl.digit_off[tid] = ex;
+            __syncthreads();
+        }
+        // stable scatter, one 1024-element tile at a time in position order
+        for (int tile = 0; tile < N; tile += kBuildThreads) {
+            const int i = tile + tid;
+            const bool valid = i < N;
+            uint32_t key = 0;
+            int32_t val = 0;
+            if (valid) {
+                if (pass == 0) {
+                    const int64_t r = load_index(idx, itype, t * tstride + i) - base;
+                    key = (r >= 0 && r < (int64_t)nrows) ? (uint32_t)r : sentinel;
+                    val = i;
+                } else {
+                    key = kin[i];
+                    val = vin[i];
+                }
+            }
+            const uint32_t digit = (key >> shift) & mask;
+            unsigned long long peers = __ballot(valid);
+            for (int bit = 0; bit < dbits; ++bit) {
+                const unsigned long long bb = __ballot(valid && ((digit >> bit) & 1u));
+                peers &= ((digit >> bit) & 1u) ? bb : ~bb;
+            }
+            const int rank = __popcll(peers & lt_mask);
+            for (int e = lane; e < 256; e += 64) sl.cnt[w][e] = 0;
+            __syncthreads();
+            if (valid && rank == 0) sl.cnt[w][digit] = __popcll(peers);
+            __syncthreads();
+            if (tid < 256) {
+                int run = sl.digit_off[tid];
+                for (int ww = 0; ww < kBuildWaves; ++ww) {
+                    const int c = sl.cnt[ww][tid];
+                    sl.cnt[ww][tid] = run;
+                    run += c;
+                }
+                sl.digit_off[tid] = run;
+            }
+            __syncthreads();
+            if (valid) {
+                const int dst = sl.cnt[w][digit] + rank;
+                kout[dst] = key;
+                vout[dst] = val;
+            }
+            __syncthreads();
+        }
+    }
+    const uint32_t* K = kbuf[passes & 1];
+    const int32_t* V = vbuf[passes & 1];
+
+    // ---- segments: one per distinct valid row; perm = sorted positions
+    if (tid == 0) sl.nvalid = 0;
+    __syncthreads();
+    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+    int32_t* perm = ix.perm + off;
+    int U = 0;
+    for (int tile = 0; tile < N; tile += kBuildThreads) {
+        const int i = tile + tid;
+        const uint32_t k = i < N ? K[i] : sentinel;
+        const bool live = i < N && k != sentinel;
+        const bool head = live && (i == 0 || K[i - 1] != k);
+        if (live) {
+            perm[i] = V[i];
+            if (i + 1 == N || K[i + 1] == sentinel) sl.nvalid = i + 1;
+        }
+        int tot;
+        const int ex = block_scan_excl(head ? 1 : 0, sl.wtot, &tot);
+        if (head) {
+            seg_start[U + ex] = i;
+            seg_row[U + ex] = k;
+        }
+        U += tot;
+    }
+    __syncthreads();
+    const int nvalid = sl.nvalid;
+    if (tid == 0) seg_start[U] = nvalid;
+    __syncthreads();
+
+    // ---- chunk and hot-segment work lists
+    int32_t* ch_beg = ix.ch_beg + off;
+    int32_t* ch_end = ix.ch_end + off;
+    uint32_t* ch_row = ix.ch_row + off;
+    int32_t* ch_slot = ix.ch_slot + off;
+    uint32_t* hot_row = ix.hot_row + off;
+    int32_t* hot_slot0 = ix.hot_slot0 + off;
+    int32_t* hot_n = ix.hot_n + off;
+    int C = 0, H = 0, HC = 0;
+    for (int tile = 0; tile < U; tile += kBuildThreads) {
+        const int s = tile + tid;
+        int beg = 0, end = 0;
+        if (s < U) { beg = seg_start[s]; end = seg_start[s + 1]; }
+        const int nch = (end - beg + kChunk - 1) / kChunk;
+        const bool hot = nch > 1;
+        int ctot, htot, hctot;
+        const int c0 = block_scan_excl(nch, sl.wtot, &ctot);
+        const int h0 = block_scan_excl(hot ? 1 : 0, sl.wtot, &htot);
+        const int hc0 = block_scan_excl(hot ? nch : 0, sl.wtot, &hctot);
+        if (s < U) {
+            const uint32_t row = seg_row[s];
+            for (int k = 0; k < nch; ++k) {
+                const int cid = C + c0 + k;
+                const int b0 = beg + k * kChunk;
+                ch_beg[cid] = b0;
+                ch_end[cid] = b0 + kChunk < end ? b0 + kChunk : end;
+                ch_row[cid] = row;
+                ch_slot[cid] = hot ? HC + hc0 + k : -1;
+            }
+            if (hot) {
+                hot_row[H + h0] = row;
+                hot_slot0[H + h0] = HC + hc0;
+                hot_n[H + h0] = nch;
+            }
+        }
+        C += ctot; H += htot; HC += hctot;
+    }
+    if (tid == 0) {
+        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
+    }
+}
+
+// Row read-modify-write of NE consecutive elements at element offset c0: row -= lr * acc,
+// one fma per element, 16-B (or 8-B) vector accesses.
+template <typename TT, int NE>
+__device__ __forceinline__ void rmw_row(TT* row, int c0, const float* acc, float lr) {
+    constexpr int BYTES = (int)sizeof(TT) * NE;
+    if constexpr (BYTES % 16 == 0) {
+        typedef Vec<TT> V;
+        constexpr int NV = BYTES / 16;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            typename V::type* p = (typename V::type*)(row + c0) + k;
+            float f[V::N];
+            V::to_f32(*p, f);
+#pragma unroll
+            for (int e = 0; e < V::N; ++e) f[e] = __builtin_fmaf(-lr, acc[k * V::N + e], f[e]);
+            *p = V::from_f32(f);
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) row[c0 + e] = from_f32<TT>(__builtin_fmaf(-lr, acc[e], to_f32(row[c0 + e])));
+    }
+}
+
+// ------------------------------------------------------------------------------ apply
+template <typename TT, typename GT, int VPR>
+struct ApplyGeom {
+    typedef Vec<GT> GV;
+    static constexpr int LPR = VPR <= 64 ? VPR : 64;
+    static constexpr int VPL = VPR <= 64 ? 1 : VPR / 64;
+    static constexpr int RPW = 64 / LPR;
+};
+
+// grad rows are fp32 or bf16; D elements = VPR vectors of 16 B of the GRAD dtype.
+template <typename TT, typename GT, int VPR>
+__global__ __launch_bounds__(256) void sgd_chunks_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int L,
+                                                         const GT* __restrict__ grad, int64_t grad_ld,
+                                                         int64_t grad_offset, float lr, float* __restrict__ partial,
+                                                         int chunks_per_block) {
+    typedef ApplyGeom<TT, GT, VPR> G;
+    typedef typename G::GV GV;
+    constexpr int NE = GV::N;
+    constexpr int D = VPR * NE;
+    const int t = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane / G::LPR, v = lane % G::LPR;
+    if (g >= G::RPW) return;
+    const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
+    const int64_t off = (int64_t)t * ix.cap;
+    const int32_t* perm = ix.perm + off;
+    const GT* gbase = grad + grad_offset + (int64_t)t * D;
+    TT* table = (TT*)tabs[t].data;
+    const int waves_per_block = blockDim.x >> 6;
+    for (int cid = blockIdx.x * chunks_per_block + w * G::RPW + g; cid < (blockIdx.x + 1) * chunks_per_block && cid < nchunks;
+         cid += waves_per_block * G::RPW) {
+        const int beg = ix.ch_beg[off + cid], end = ix.ch_end[off + cid];
+        float acc[G::VPL][NE];
+#pragma unroll
+        for (int j = 0; j < G::VPL; ++j)
+#pragma unroll
+            for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
+        for (int i = beg; i < end; i += 4) {
+            typename GV::type gv[4][G::VPL];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i + u < end) {
+                    const int64_t b = perm[i + u] / L;
+                    const GT* gr = gbase + b * grad_ld;
+#pragma unroll
+                    for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i + u < end) {
+#pragma unroll
+                    for (int j = 0; j < G::VPL; ++j) {
+                        float f[NE];
+                        GV::to_f32(gv[u][j], f);
+#pragma unroll
+                        for (int e = 0; e < NE; ++e) acc[j][e] += f[e];
+                    }
+                }
+            }
+        }
+        const int slot = ix.ch_slot[off + cid];
+        if (slot < 0) {
+            TT* row = table + (int64_t)ix.ch_row[off + cid] * D;
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j) rmw_row<TT, NE>(row, (v + j * 64) * NE, acc[j], lr);
+        } else {
+            float* pr = partial + ((int64_t)t * ix.hot_cap + slot) * D;
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j)
+#pragma unroll
+                for (int e = 0; e < NE; ++e) pr[(v + j * 64) * NE + e] = acc[j][e];
+        }
+    }
+}
+
+template <typename TT, typename GT, int VPR>
+__global__ __launch_bounds__(256) void sgd_hot_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, float lr,
+                                                      const float* __restrict__ partial) {
+    typedef ApplyGeom<TT, GT, VPR> G;
+    constexpr int NE = Vec<GT>::N;
+    constexpr int D = VPR * NE;
+    const int t = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane / G::LPR, v = lane % G::LPR;
+    if (g >= G::RPW) return;
+    const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
+    const int64_t off = (int64_t)t * ix.cap;
+    TT* table = (TT*)tabs[t].data;
+    const int per_block = (blockDim.x >> 6) * G::RPW;
+    for (int h = blockIdx.x * per_block + w * G::RPW + g; h < nhot; h += gridDim.x * per_block) {
+        const int s0 = ix.hot_slot0[off + h], n = ix.hot_n[off + h];
+        const float* pr = partial + ((int64_t)t * ix.hot_cap + s0) * D;
+        TT* row = table + (int64_t)ix.hot_row[off + h] * D;
+#pragma unroll
+        for (int j = 0; j < G::VPL; ++j) {
+            float acc[NE];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) acc[e] = 0.0f;
+            for (int k = 0; k < n; ++k)
+#pragma unroll
+                for (int e = 0; e < NE; ++e) acc[e] += pr[(int64_t)k * D + (v + j * 64) * NE + e];
+            rmw_row<TT, NE>(row, (v + j * 64) * NE, acc, lr);
+        }
+    }
+}
+
+// Generic (any D) versions: one thread per element column, loops over the chunk.
+template <typename TT, typename GT>
+__global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,
+                                                         const GT* __restrict__ grad, int64_t grad_ld,
+                                                         int64_t grad_offset, float lr, float* __restrict__ partial) {
+    const int t = blockIdx.y;
+    const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
+    const int64_t off = (int64_t)t * ix.cap;
+    const int64_t total = (int64_t)nchunks * D;
+    TT* table = (TT*)tabs[t].data;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int cid = (int)(e / D), c = (int)(e % D);
+        const int beg = ix.ch_beg[off + cid], end = ix.ch_end[off + cid];
+        float acc = 0.0f;
+        for (int i = beg; i < end; ++i) {
+            const int64_t b = ix.perm[off + i] / L;
+            acc += to_f32(grad[b * grad_ld + grad_offset + (int64_t)t * D + c]);
+        }
+        const int slot = ix.ch_slot[off + cid];
+        if (slot < 0) {
+            TT* row = table + (int64_t)ix.ch_row[off + cid] * D;
+            row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
+        } else {
+            partial[((int64_t)t * ix.hot_cap + slot) * D + c] = acc;
+        }
+    }
+}
+
+template <typename TT>
+__global__ __launch_bounds__(256) void sgd_hot_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, float lr,
+                                                      const float* __restrict__ partial) {
+    const int t = blockIdx.y;
+    const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
+    const int64_t off = (int64_t)t * ix.cap;
+    const int64_t total = (int64_t)nhot * D;
+    TT* table = (TT*)tabs[t].data;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int h = (int)(e / D), c = (int)(e % D);
+        const int s0 = ix.hot_slot0[off + h], n = ix.hot_n[off + h];
+        float acc = 0.0f;
+        for (int k = 0; k < n; ++k) acc += partial[((int64_t)t * ix.hot_cap + s0 + k) * D + c];
+        TT* row = table + (int64_t)ix.hot_row[off + h] * D;
+        row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
+    }
+}
+
+// Non-deterministic: every lookup adds -lr * grad straight into its row (fp32 tables).
+template <typename GT>
+__global__ __launch_bounds__(256) void sgd_atomic_kernel(TableDesc* __restrict__ tabs, int ntab, int D,
+                                                         const void* __restrict__ idx, int itype, int64_t tstride,
+                                                         int base, int B, int L, const GT* __restrict__ grad,
+                                                         int64_t grad_ld, int64_t grad_offset, float lr,
+                                                         unsigned* __restrict__ err) {
+    const int64_t N = (int64_t)B * L;
+    const int64_t total = (int64_t)ntab * N * D;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e % D);
+        const int64_t item = e / D;
+        const int t = (int)(item / N);
+        const int64_t p = item - (int64_t)t * N;
+        const int64_t r = load_index(idx, itype, t * tstride + p) - base;
+        if (r < 0 || r >= tabs[t].nrows) {
+            if (c == 0) raise_index_error(err);
+            continue;
+        }
+        const float gval = to_f32(grad[(p / L) * grad_ld + grad_offset + (int64_t)t * D + c]);
+        unsafeAtomicAdd((float*)tabs[t].data + r * D + c, -lr * gval);
+    }
+}
+
+// ------------------------------------------------------------------------ launchers
+size_t indexer_lds_bytes() { return sizeof(uint32_t) * 2 * kLdsSortMax + sizeof(int32_t) * 2 * kLdsSortMax; }
+int indexer_chunk() { return kChunk; }
+
+int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx,
+                         int itype, int64_t tstride, int base, int B, int L) {
+    if (T_ == 0) return DLRM_OK;
+    hipStream_t s = ctx_stream(ctx);
+    const int64_t N = (int64_t)B * L;
+    if (N <= kLdsSortMax)
+        hipLaunchKernelGGL(indexer_build_kernel<true>, dim3(T_), dim3(kBuildThreads), indexer_lds_bytes(), s, ix, tabs,
+                           idx, itype, tstride, base, B, L, ctx_error_word(ctx));
+    else
+        hipLaunchKernelGGL(indexer_build_kernel<false>, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, idx, itype,
+                           tstride, base, B, L, ctx_error_word(ctx));
+    return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
+}
+
+template <typename TT, typename GT, int VPR>
+static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
+                             int64_t grad_ld, int64_t grad_offset, float lr, float* partial, int64_t N) {
+    typedef ApplyGeom<TT, GT, VPR> G;
+    const int per_block = 4 * G::RPW * 4;  // 4 waves x RPW groups x 4 rounds
+    const int64_t gx = (N + per_block - 1) / per_block;
+    hipLaunchKernelGGL((sgd_chunks_kernel<TT, GT, VPR>), dim3((unsigned)(gx < 1 ? 1 : gx), T_), dim3(256), 0, s, ix,
+                       tabs, L, (const GT*)grad, grad_ld, grad_offset, lr, partial, per_block);
+    const int64_t hx = (ix.hot_cap + 4 * G::RPW - 1) / (4 * G::RPW);
+    hipLaunchKernelGGL((sgd_hot_kernel<TT, GT, VPR>), dim3((unsigned)(hx < 1 ? 1 : (hx > 64 ? 64 : hx)), T_), dim3(256),
+                       0, s, ix, tabs, lr, partial);
+}
+
+template <typename TT, typename GT>
+static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L,
+                           const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, float* partial, int64_t N) {
+#define DLRM_CASE(V) \
+    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, partial, N); return true;
+    switch (vpr) {
+        DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64) DLRM_CASE(128)
+        default: return false;
+    }
+#undef DLRM_CASE
+}
+
+int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T_, int D,
+                     int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
+                     float lr, float* partial) {
+    if (T_ == 0 || N == 0) return DLRM_OK;
+    hipStream_t s = ctx_stream(ctx);
+    const int gesz = gdtype == DLRM_F32 ? 4 : 2;
+    const bool aligned = tabs_aligned16 && (uintptr_t)grad % 16 == 0 && (grad_ld * gesz) % 16 == 0 &&
+                         (grad_offset * gesz) % 16 == 0 && (D * gesz) % 16 == 0;
+    bool done = false;
+    if (aligned) {
+        const int vpr = D * gesz / 16;
+        if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
+            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, partial, N);
+        else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32)
+            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, partial, N);
+        else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16)
+            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, partial, N);
+        else
+            done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, partial, N);
+    }
+    if (!done) {
+        const int64_t gx0 = (N * D + 255) / 256;
+        const unsigned gx = (unsigned)(gx0 < 1 ? 1 : (gx0 > 4096 ? 4096 : gx0));
+        const int64_t hx0 = (ix.hot_cap * D + 255) / 256;
+        const unsigned hx = (unsigned)(hx0 < 1 ? 1 : (hx0 > 1024 ? 1024 : hx0));
+#define DLRM_SCALAR(TT, GT)                                                                                        \
+    hipLaunchKernelGGL((sgd_chunks_scalar<TT, GT>), dim3(gx, T_), dim3(256), 0, s, ix, tabs, D, L, (const GT*)grad, \
+                       grad_ld, grad_offset, lr, partial);                                                          \
+    hipLaunchKernelGGL((sgd_hot_scalar<TT>), dim3(hx, T_), dim3(256), 0, s, ix, tabs, D, lr, partial);
+        if (tdtype == DLRM_F32 && gdtype == DLRM_F32) { DLRM_SCALAR(float, float) }
+        else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32) { DLRM_SCALAR(uint16_t, float) }
+        else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16) { DLRM_SCALAR(float, uint16_t) }
+        else { DLRM_SCALAR(uint16_t, uint16_t) }
+#undef DLRM_SCALAR
+    }
+    return ctx_hip(ctx, hipGetLastError(), "sgd_apply launch");
+}
+
+int launch_sgd_atomic(dlrm_ctx* ctx, TableDesc* tabs, int T_, int D, const void* idx, int itype, int64_t tstride,
+                      int base, int B, int L, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
+                      float lr) {
+    if (T_ == 0 || B == 0) return DLRM_OK;
+    hipStream_t s = ctx_stream(ctx);
+    const int64_t total = (int64_t)T_ * B * L * D;
+    int64_t g = (total + 255) / 256;
+    const int64_t cap = (int64_t)ctx_num_cus(ctx) * 16;
+    if (g > cap) g = cap;
+    if (gdtype == DLRM_F32)
+        hipLaunchKernelGGL(sgd_atomic_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, tabs, T_, D, idx, itype, tstride,
+                           base, B, L, (const float*)grad, grad_ld, grad_offset, lr, ctx_error_word(ctx));
+    else
+        hipLaunchKernelGGL(sgd_atomic_kernel<uint16_t>, dim3((unsigned)g), dim3(256), 0, s, tabs, T_, D, idx, itype,
+                           tstride, base, B, L, (const uint16_t*)grad, grad_ld, grad_offset, lr, ctx_error_word(ctx));
+    return ctx_hip(ctx, hipGetLastError(), "sgd_atomic launch");
+}
+
+}  // namespace dlrm

@@ -1,0 +1,120 @@
+"""The hot path as one preallocated training-step engine.
+
+One `HotPath.step(x, indices, dout)` = what DLRM.jl's train! loop (src/train/train.jl:215-227)
+does for the sparse half of the model on one batch:
+
+    ys  = maplookup(PreallocationStrategy(d), tables, sparse)      model.jl:161
+    out = interaction(x, ys)                                       model.jl:163
+    (top MLP + loss produce dout = dLoss/dout: out of scope, supplied by the caller)
+    dx, dt = dot_back(dot, dout, T, d, padding)                    interact.jl:442-445
+    update!(Descent(lr), tables, maplookup_pullback(dt), indexers) train.jl:283-290
+
+All buffers are allocated once; a step issues 4 kernel launches on the current stream
+(lookup, interaction fwd, interaction bwd, indexer sort) + 2 for the update, with no
+host synchronisation, so the whole step can be captured in a torch.cuda graph.  With
+`overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a
+side stream concurrently with the lookup and the interaction.
+"""
+import torch
+
+from . import _lib
+from .embedding import EmbeddingTableSet, PackedIndices
+from .interact import interaction_sizes
+from .runtime import dtype_code, ptr
+from .update import SparseIndexer
+
+
+class HotPath:
+    def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
+                 overlap_indexer=False, pad_to=1):
+        self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
+        self.B, self.L = int(batch), int(lookups)
+        self.T, self.D = len(self.ts), self.ts.D
+        self.d = self.D  # dense vector length == feature size (model.jl:220)
+        self.F = self.T + 1
+        self.lr = float(lr)
+        self.index_base = int(index_base)
+        self.deterministic = deterministic
+        _, self.width, self.padding = interaction_sizes(self.d, self.F, pad_to)
+        dev, dt = self.ts.device, self.ts.dtype
+        self.ys = torch.empty((self.B, self.F * self.D), dtype=dt, device=dev)
+        self.out = torch.empty((self.B, self.width), dtype=dt, device=dev)
+        self.dx = torch.empty((self.B, self.d), dtype=torch.float32, device=dev)
+        self.dt = torch.empty((self.B, self.F * self.d), dtype=torch.float32, device=dev)
+        self.indexer = SparseIndexer(self.T, self.B * self.L, dev) if deterministic else None
+        self.ctx = self.ts.ctx
+        self.lib = self.ctx.lib
+        self.dcode = dtype_code(dt)
+        self.overlap_indexer = overlap_indexer and deterministic
+        self._side = torch.cuda.Stream(device=dev) if self.overlap_indexer else None
+        self._indexer_done = None
+
+    # -- pieces --------------------------------------------------------------------------
+    def _check(self, rc):
+        if rc != _lib.OK:
+            self.ctx.check(rc)
+
+    def lookup(self, idx):
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_maplookup(h, self.ts.handle, ptr(idx.data), idx.itype, idx.stride, self.index_base,
+                                            self.B, self.L, ptr(self.ys), self.ys.stride(0), self.d))
+
+    def interact_fwd(self, x):
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_interact_fwd(h, self.dcode, self.d, self.F, self.B, ptr(x), x.stride(0),
+                                               ptr(self.ys), self.ys.stride(0), ptr(self.out), self.out.stride(0),
+                                               self.padding))
+
+    def build_indexer(self, idx):
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_indexer_build(h, self.indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
+                                                idx.stride, self.index_base, self.B, self.L))
+
+    def interact_bwd(self, dout):
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_interact_bwd(h, self.dcode, self.d, self.F, self.B, ptr(dout), dout.stride(0),
+                                               self.padding, ptr(self.ys), self.ys.stride(0), ptr(self.dx),
+                                               self.dx.stride(0), ptr(self.dt), self.dt.stride(0)))
+
+    def sgd_update(self, idx, prebuilt):
+        h = self.ctx.bind()
+        flags = 0 if self.deterministic else _lib.UPDATE_ATOMIC
+        if prebuilt:
+            flags |= _lib.UPDATE_PREBUILT
+        self._check(self.lib.dlrm_sgd_update(h, self.ts.handle, self.indexer.handle if self.indexer else None, flags,
+                                             ptr(idx.data), idx.itype, idx.stride, self.index_base, self.B, self.L,
+                                             ptr(self.dt), _lib.F32, self.dt.stride(0), self.d, self.lr))
+
+    # -- step --------------------------------------------------------------------------
+    def forward(self, x, idx):
+        if self.overlap_indexer:
+            main = torch.cuda.current_stream(self.ts.device)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self.build_indexer(idx)
+                self._indexer_done = torch.cuda.Event()
+                self._indexer_done.record(self._side)
+        self.lookup(idx)
+        self.interact_fwd(x)
+        return self.out
+
+    def backward(self, idx, dout):
+        self.interact_bwd(dout)
+        prebuilt = False
+        if self.overlap_indexer and self._indexer_done is not None:
+            torch.cuda.current_stream(self.ts.device).wait_event(self._indexer_done)
+            prebuilt = True
+        self.sgd_update(idx, prebuilt)
+        return self.dx
+
+    def step(self, x, idx, dout):
+        self.forward(x, idx)
+        return self.backward(idx, dout)
+
+    def check_bounds(self):
+        self.ctx.check_bounds()
+
+
+def packed(indices_tensor):
+    """[T][B] or [T][B][L] int32/int64 device tensor -> PackedIndices (no copy)."""
+    return PackedIndices(indices_tensor)

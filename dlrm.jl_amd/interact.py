@@ -1,0 +1,100 @@
+"""DotInteraction — the pairwise-dot feature interaction (src/model/interact.jl:294-489).
+
+`dot = DotInteraction(); out = dot(x, ys)` runs fast_vcat + process_batches on the GPU
+(one MFMA kernel); `dot_back(dot, Δ, t, xlen, padding)` runs process_batches_back + sumavx
+(one MFMA kernel); `rrule(dot, x, ys)` pairs them like ChainRulesCore.rrule (:438-447).
+
+Shapes (torch, row-major = the transpose of the Julia matrices):
+  x   [B][d]                    dense bottom-MLP output
+  ys  [B][P + D*T], P == d      maplookup(PreallocationStrategy(d)) output; x is copied in
+  out [B][d + F(F-1)/2 + pad]   F = 1 + T, pad from POST_INTERACTION_PAD_TO_MUL (model.jl:32)
+  dt  [B][F*d] float32          dt_reshaped, x rows included (:428-435)
+"""
+import torch
+
+from .runtime import context, dtype_code, ptr
+
+POST_INTERACTION_PAD_TO_MUL = 1  # model.jl:32
+
+
+def cdiv(x, y):
+    return 1 + (x - 1) // y
+
+
+def up_to_mul_of(x, y):
+    return y * cdiv(x, y)
+
+
+def interaction_sizes(d, F, pad_to=POST_INTERACTION_PAD_TO_MUL):
+    """(unpadded, padded, padding) exactly as process_batches computes them (:449-456)."""
+    unpadded = (F * F - F) // 2 + d
+    padded = up_to_mul_of(unpadded, pad_to)
+    return unpadded, padded, padded - unpadded
+
+
+class DotInteraction:
+    """DotInteraction (interact.jl:369-411).  Holds no per-thread scratchpads: the kernel keeps
+    each sample's Gram tile in MFMA accumulators and its packed row in LDS."""
+
+    def __init__(self, pad_to=POST_INTERACTION_PAD_TO_MUL):
+        self.pad_to = pad_to
+
+    def __call__(self, x, ys, *, return_t=False, out=None):
+        if x.dim() != 2 or ys.dim() != 2 or x.shape[0] != ys.shape[0]:
+            raise ValueError("DotInteraction: x [B][d] and ys [B][d + D*T] expected")
+        if x.dtype != ys.dtype:
+            raise TypeError("DotInteraction: x and ys must share a dtype")
+        B, d = x.shape
+        if ys.shape[1] % d != 0:
+            # reshape(combined, (d, :, batchsize)) in the reference requires this (:397)
+            raise ValueError(f"ys width {ys.shape[1]} is not a multiple of d={d}")
+        if x.stride(1) != 1 or ys.stride(1) != 1:
+            raise ValueError("DotInteraction: rows must be contiguous")
+        F = ys.shape[1] // d
+        _, padded, padding = interaction_sizes(d, F, self.pad_to)
+        if out is None:
+            out = torch.empty((B, padded), dtype=x.dtype, device=x.device)
+        ctx = context(x.device)
+        ctx.check(ctx.lib.dlrm_interact_fwd(ctx.bind(), dtype_code(x.dtype), d, F, B, ptr(x), x.stride(0), ptr(ys),
+                                            ys.stride(0), ptr(out), out.stride(0), padding))
+        if return_t:
+            return out, ys, padding
+        return out
+
+
+def dot_back(dot, delta, t, xlen, padding, *, dx=None, dt=None):
+    """dot_back(dot, Δ, T, xlen, padding) -> (dx, dt_reshaped)   (interact.jl:415-436).
+    bf16 Δ is handled like the reference (converted to fp32; dx and dt are fp32)."""
+    B = delta.shape[0]
+    d = xlen
+    F = t.shape[1] // d
+    if dx is None:
+        dx = torch.empty((B, d), dtype=torch.float32, device=delta.device)
+    if dt is None:
+        dt = torch.empty((B, F * d), dtype=torch.float32, device=delta.device)
+    if delta.dtype != t.dtype:
+        raise TypeError("dot_back: Δ and T must share a dtype")
+    ctx = context(delta.device)
+    ctx.check(ctx.lib.dlrm_interact_bwd(ctx.bind(), dtype_code(delta.dtype), d, F, B, ptr(delta), delta.stride(0),
+                                        padding, ptr(t), t.stride(0), ptr(dx), dx.stride(0), ptr(dt), dt.stride(0)))
+    return dx, dt
+
+
+def rrule(dot, x, ys):
+    """ChainRulesCore.rrule(dot::DotInteraction, X, Y) (interact.jl:438-447)."""
+    forward, t, padding = dot(x, ys, return_t=True)
+    xlen = x.shape[1]
+
+    def dot_pullback(delta):
+        dx, dy = dot_back(dot, delta, t, xlen, padding)
+        return None, dx, dy
+
+    return forward, dot_pullback
+
+
+def fast_vcat(x, ys):
+    """fast_vcat(x, ys) (interact.jl:271-281): copy x into the top rows reserved in ys.
+    DotInteraction already fuses this copy into its kernel; this standalone form exists for
+    API parity (a plain device copy)."""
+    ys[:, : x.shape[1]].copy_(x)
+    return ys

@@ -1,0 +1,82 @@
+"""Device context: one dlrm_ctx per GPU, bound to torch's current stream at each call.
+
+Mirrors the ABI's threading rule (one ctx = one device + one stream, not re-entrant):
+every call re-binds the ctx to `torch.cuda.current_stream()`, so kernels are ordered with
+the surrounding torch work and can be captured by torch.cuda graphs.
+"""
+import ctypes
+import threading
+
+import torch
+
+from . import _lib
+
+_contexts = {}
+_lock = threading.Lock()
+
+
+class Context:
+    def __init__(self, device_index):
+        self.lib = _lib.load()
+        self.device = device_index
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device_index):
+            _lib.check(self.lib.dlrm_ctx_create(device_index, None, ctypes.byref(h)))
+        self.handle = h
+
+    def bind(self):
+        """Returns the ctx handle bound to torch's current stream on this device."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.lib.dlrm_ctx_set_stream(self.handle, ctypes.c_void_p(stream))
+        return self.handle
+
+    def check(self, rc):
+        _lib.check(rc, self.handle)
+
+    def check_bounds(self):
+        """Synchronises and raises BoundsError if a kernel skipped an out-of-range index."""
+        self.check(self.lib.dlrm_check_bounds(self.bind()))
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.lib.dlrm_ctx_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def context(device=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("dlrm.jl_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback for the hot path")
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    else:
+        idx = int(device)
+    with _lock:
+        ctx = _contexts.get(idx)
+        if ctx is None:
+            ctx = _contexts[idx] = Context(idx)
+        return ctx
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return _lib.F32
+    if dt == torch.bfloat16:
+        return _lib.BF16
+    raise TypeError(f"unsupported dtype {dt}: the hot path computes in float32 or bfloat16")
+
+
+def itype_code(dt):
+    if dt == torch.int32:
+        return _lib.I32
+    if dt == torch.int64:
+        return _lib.I64
+    raise TypeError(f"unsupported index dtype {dt}: int32 or int64")

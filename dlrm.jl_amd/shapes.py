@@ -1,0 +1,35 @@
+"""Workload shapes of the DLRM hot path (BASELINE.json configs).
+
+Table row counts are the reference's own constants (src/data/criteo.jl:350-406).
+"""
+
+# src/data/criteo.jl:350-377
+KAGGLE_EMBEDDING_SIZES = [
+    1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194, 27,
+    14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572,
+]
+
+# src/data/criteo.jl:379-406
+TERABYTE_EMBEDDING_SIZES = [
+    227605432, 39060, 17295, 7424, 20265, 3, 7122, 1543, 63, 130229467, 3067956, 405282, 10,
+    2209, 11938, 155, 4, 976, 14, 292775614, 40790948, 187188510, 590152, 12973, 108, 36,
+]
+
+# name -> workload description (bench.py's config.workload names one of these)
+WORKLOADS = {
+    # configs[0]: 7 tables x 1000 x 16 (+ dense = 8 features), B=128 — golden HDF5 (parity only)
+    "golden-single": dict(rows=[1000] * 7, dim=16, batch=128, lookups=1, dtype="f32"),
+    "golden-multi": dict(rows=[1000] * 7, dim=16, batch=128, lookups=10, dtype="f32"),
+    # configs[1]: Criteo-Kaggle shape, dim 16, batch 2048, fp32 (gather/scatter)
+    "kaggle-d16-b2048": dict(rows=KAGGLE_EMBEDDING_SIZES, dim=16, batch=2048, lookups=1, dtype="f32"),
+    # BASELINE.json metric: 26 tables x 128-dim, bs=2048 (Kaggle rows), fp32, fwd+bwd
+    "kaggle-d128-b2048": dict(rows=KAGGLE_EMBEDDING_SIZES, dim=128, batch=2048, lookups=1, dtype="f32"),
+    # configs[2]: 26 tables, dim 128, batch 8192, bf16 — MFMA interaction
+    "kaggle-d128-b8192-bf16": dict(rows=KAGGLE_EMBEDDING_SIZES, dim=128, batch=8192, lookups=1, dtype="bf16"),
+    # configs[4]: pooled mode, 64 tables x dim 256, hot-row skew (rows per table: 1M)
+    "pooled-64x256-l10": dict(rows=[1_000_000] * 64, dim=256, batch=2048, lookups=10, dtype="f32", zipf=1.2),
+}
+
+
+def table_bytes(rows, dim, esize):
+    return sum(rows) * dim * esize

@@ -1,0 +1,163 @@
+"""Sparse embedding gradients and the SGD scatter update.
+
+Mirrors EmbeddingTables' training API as DLRM.jl calls it:
+  * the maplookup pullback -> one `SparseEmbeddingUpdate(delta, indices)` per table
+    (test/model/embedding_update.jl:35-40, test/train/backprop.jl:147-158);
+  * `SparseIndexer()` per table (src/train/train.jl:276-281);
+  * `update!(Descent(lr), tables, grads, indexers; num_splits, nthreads)`
+    (src/train/train.jl:283-290) -> `update_` here (Python has no `!`).
+The deterministic GPU path dedupes each table's indices with a stable sort and writes every
+touched row once; `deterministic=False` uses float atomics instead.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .embedding import EmbeddingTableSet, PackedIndices, as_table_set
+from .runtime import context, dtype_code, ptr
+
+
+class Descent:
+    """Flux.Descent(η): plain SGD, w .-= η * g (default η = 0.1 as in Flux)."""
+
+    def __init__(self, eta=0.1):
+        self.eta = float(eta)
+
+    def __repr__(self):
+        return f"Descent({self.eta})"
+
+
+class SparseEmbeddingUpdate:
+    """SparseEmbeddingUpdate{Static{D}}(delta, indices): the gradient of one table.
+
+    `delta` is a [B][D] view (column block of the interaction's dt); `grad`, `grad_offset`
+    keep the parent matrix so that all tables can be updated in one launch."""
+
+    def __init__(self, grad, grad_offset, featuresize, indices, table_index):
+        self.grad = grad
+        self.grad_offset = int(grad_offset)
+        self.featuresize = int(featuresize)
+        self.indices = indices  # PackedIndices of ALL tables (row `table_index` is this table's)
+        self.table_index = int(table_index)
+
+    @property
+    def delta(self):
+        return self.grad[:, self.grad_offset:self.grad_offset + self.featuresize]
+
+    def uncompress(self, nrows, *, index_base=1):
+        """uncompress(update, nrows) (test/train/backprop.jl:156): dense [nrows][D] scatter-add.
+        A plain torch scatter for tests/inspection; the training path never materialises it."""
+        idx = self.indices.data[self.table_index].to(torch.int64) - index_base
+        L = self.indices.L
+        g = self.delta.to(torch.float32)
+        if L > 1:
+            g = g.repeat_interleave(L, dim=0)
+        out = torch.zeros((nrows, self.featuresize), dtype=torch.float32, device=g.device)
+        out.index_add_(0, idx, g)
+        return out
+
+
+def maplookup_pullback(strategy_prealloc, tables, sparse, dy):
+    """Pullback of maplookup(PreallocationStrategy(P), tables, sparse) given dy [B][P + D*T]
+    (e.g. dt_reshaped from dot_back): views, no arithmetic (the rows 1:P belong to x)."""
+    ts = as_table_set(tables)
+    idx = sparse if isinstance(sparse, PackedIndices) else PackedIndices(sparse, device=ts.device)
+    return [SparseEmbeddingUpdate(dy, strategy_prealloc + t * ts.D, ts.D, idx, t) for t in range(len(ts))]
+
+
+class SparseIndexer:
+    """SparseIndexer(): dedupe state for `update_`.  One object serves a whole table set (the
+    reference keeps one per table); sized for `capacity` lookups per table."""
+
+    def __init__(self, num_tables, capacity, device=None):
+        self.ctx = context(device)
+        self.num_tables = int(num_tables)
+        self.capacity = int(capacity)
+        h = ctypes.c_void_p()
+        self.ctx.check(self.ctx.lib.dlrm_indexer_create(self.ctx.bind(), self.num_tables, self.capacity,
+                                                        ctypes.byref(h)))
+        self.handle = h
+        self._built_from = None
+
+    def build(self, tables, indices, *, index_base=1):
+        """Dedupes `indices` (asynchronous).  May run on a side stream during the forward pass;
+        pass prebuilt=True to update_ afterwards."""
+        ts = as_table_set(tables)
+        idx = indices if isinstance(indices, PackedIndices) else PackedIndices(indices, device=ts.device)
+        self.ctx.check(self.ctx.lib.dlrm_indexer_build(self.ctx.bind(), self.handle, ts.handle, ptr(idx.data),
+                                                       idx.itype, idx.stride, index_base, idx.B, idx.L))
+        self._built_from = idx
+        return self
+
+    def unique_rows(self, table):
+        """Sorted 0-based unique rows touched in `table` by the last build (synchronises)."""
+        n = ctypes.c_int64()
+        cap = self.capacity
+        rows = (ctypes.c_int64 * max(cap, 1))()
+        self.ctx.check(self.ctx.lib.dlrm_indexer_read(self.ctx.bind(), self.handle, table, ctypes.byref(n), rows,
+                                                      None, None, cap))
+        return list(rows[: n.value])
+
+    def segments(self, table):
+        """(unique_rows, positions, seg_start) of `table`: positions sorted by row, ascending within a row."""
+        n = ctypes.c_int64()
+        cap = self.capacity
+        rows = (ctypes.c_int64 * max(cap, 1))()
+        pos = (ctypes.c_int64 * max(cap, 1))()
+        seg = (ctypes.c_int64 * (cap + 1))()
+        self.ctx.check(self.ctx.lib.dlrm_indexer_read(self.ctx.bind(), self.handle, table, ctypes.byref(n), rows, pos,
+                                                      seg, cap))
+        U = n.value
+        segs = list(seg[: U + 1])
+        nv = segs[U] if U >= 0 else 0
+        return list(rows[:U]), list(pos[:nv]), segs
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.ctx.lib.dlrm_indexer_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, index_base=1, deterministic=True,
+            prebuilt=False, check_bounds=True):
+    """EmbeddingTables.update!(opt, tables, grads, indexers; num_splits, nthreads).
+
+    `grads` are the SparseEmbeddingUpdates of maplookup_pullback (they share one gradient
+    matrix and one PackedIndices, so all tables update in one launch).  num_splits/nthreads
+    are accepted for signature parity; the GPU decomposition is chunk-based.
+    Tables are mutated in place."""
+    del num_splits, nthreads
+    if not isinstance(opt, Descent):
+        raise TypeError("update_ implements Descent (plain SGD), the optimizer DLRM.jl trains with")
+    ts = as_table_set(tables)
+    if len(grads) != len(ts):
+        raise ValueError(f"{len(grads)} gradients for {len(ts)} tables")
+    g0 = grads[0]
+    for t, g in enumerate(grads):
+        if (g.grad.data_ptr() != g0.grad.data_ptr() or g.indices is not g0.indices or g.table_index != t or
+                g.grad_offset != g0.grad_offset + t * ts.D):
+            raise ValueError("update_ expects the per-table views produced by maplookup_pullback")
+    grad = g0.grad
+    if grad.stride(1) != 1:
+        raise ValueError("gradient rows must be contiguous")
+    idx = g0.indices
+    flags = 0
+    ix = None
+    if deterministic:
+        if indexers is None:
+            indexers = SparseIndexer(len(ts), idx.B * idx.L, ts.device)
+        ix = indexers
+        if prebuilt:
+            flags |= _lib.UPDATE_PREBUILT
+    else:
+        flags |= _lib.UPDATE_ATOMIC
+    ctx = ts.ctx
+    ctx.check(ctx.lib.dlrm_sgd_update(ctx.bind(), ts.handle, ix.handle if ix is not None else None, flags,
+                                      ptr(idx.data), idx.itype, idx.stride, index_base, idx.B, idx.L, ptr(grad),
+                                      dtype_code(grad.dtype), grad.stride(0), g0.grad_offset, opt.eta))
+    if check_bounds:
+        ctx.check_bounds()
+    return tables

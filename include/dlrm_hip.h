@@ -1,0 +1,158 @@
+/*
+ * dlrm_hip.h — C ABI of the MI355X (gfx950) DLRM embedding + feature-interaction hot path.
+ *
+ * This is the drop-in boundary for darchr/DLRM.jl.  Every entry point replaces one operator
+ * of the reference's hot path (citations are /root/reference paths):
+ *
+ *   dlrm_maplookup        EmbeddingTables.maplookup(PreallocationStrategy(P), tables, sparse)
+ *                         called at src/model/model.jl:161; semantics pinned by
+ *                         test/model/embedding_update.jl:23-33, test/model/interact.jl:168-171,
+ *                         test/integration.jl:10-11 (the package itself is un-vendored).
+ *   dlrm_interact_fwd     (dot::DotInteraction)(x, ys)           src/model/interact.jl:394-411
+ *                         = fast_vcat (:271-281) + process_batches (:449-467)
+ *                           + process_slice! (:338-362) + triangular_slice_kernel! (:64-75)
+ *   dlrm_interact_bwd     dot_back / process_batches_back        src/model/interact.jl:415-489
+ *                         (fused unpack :154-173, gemmavx! :318-326, sumavx :329-336)
+ *   dlrm_indexer_*        EmbeddingTables.SparseIndexer()        src/train/train.jl:276-281
+ *   dlrm_sgd_update       EmbeddingTables.update!(Descent(lr), tables, grads, indexers;
+ *                         num_splits, nthreads)                  src/train/train.jl:283-290
+ *                         (grads = maplookup pullback = SparseEmbeddingUpdate views of dt,
+ *                         test/train/backprop.jl:147-158, src/validation.jl:125-146)
+ *
+ * Conventions
+ *  - All tensors are caller-owned DEVICE memory (from dlrm_malloc, hipMalloc or torch).
+ *    Nothing on a launch path allocates or synchronises, so every launching call can be
+ *    captured into a hipGraph.
+ *  - Layout: a Julia column-major (D, N) matrix is C row-major [N][D].  The lookup output
+ *    (P + D*T) x B is C [B][out_ld] with table t at columns out_offset + t*D; the interaction
+ *    output (d + F(F-1)/2 + padding) x B is C [B][out_ld].
+ *  - Indices are int32 or int64, laid out [T][batch*lookups] with a per-table stride
+ *    (sample-major within a table: position p = b*lookups + k, as load_inputs reshapes them,
+ *    src/data/criteo.jl:551-557).  index_base is 1 for Julia / DACLoader indices, 0 for
+ *    PyTorch / HDF5 indices.
+ *  - Errors: every function returns a dlrm_status (0 = OK, negative = error) and no C++
+ *    exception crosses the ABI.  dlrm_last_error(ctx) describes the last failure.
+ *    Out-of-range indices never fault: kernels skip them and raise a device-side flag that
+ *    dlrm_check_bounds() turns into DLRM_E_INDEX (the reference throws BoundsError).
+ *  - Threading: one ctx = one device + one stream; calls are asynchronous on that stream;
+ *    a ctx must not be used from two host threads at once.
+ */
+#ifndef DLRM_HIP_H
+#define DLRM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLRM_HIP_ABI_VERSION 1
+
+typedef enum {
+    DLRM_OK = 0,
+    DLRM_E_ARG = -1,         /* invalid argument (shape, null pointer, dtype)          */
+    DLRM_E_HIP = -2,         /* HIP runtime error                                       */
+    DLRM_E_INDEX = -3,       /* an index was outside [index_base, index_base + nrows)   */
+    DLRM_E_UNSUPPORTED = -4, /* valid request this build does not implement             */
+    DLRM_E_NOMEM = -5,       /* device allocation failed                                */
+    DLRM_E_STATE = -6        /* object used in the wrong state (e.g. indexer not built) */
+} dlrm_status;
+
+typedef enum { DLRM_F32 = 0, DLRM_BF16 = 1 } dlrm_dtype;
+typedef enum { DLRM_I32 = 0, DLRM_I64 = 1 } dlrm_itype;
+
+/* dlrm_sgd_update flags */
+#define DLRM_UPDATE_ATOMIC 1u   /* float atomics straight into the rows: fastest to launch,
+                                   NOT bitwise reproducible (fp32 tables only)            */
+#define DLRM_UPDATE_PREBUILT 2u /* the indexer was already built from these indices by
+                                   dlrm_indexer_build (e.g. on a side stream during the
+                                   forward pass); skip rebuilding it                     */
+
+typedef struct dlrm_ctx dlrm_ctx;         /* device + stream + error word                  */
+typedef struct dlrm_tables dlrm_tables;   /* Vector{SimpleEmbedding{Static{D}}} on device  */
+typedef struct dlrm_indexer dlrm_indexer; /* Vector{SparseIndexer}: per-table dedupe state */
+
+/* ---- context ---------------------------------------------------------------------- */
+int dlrm_abi_version(void);
+int dlrm_ctx_create(int device, void* stream /* hipStream_t, NULL = default */, dlrm_ctx** out);
+int dlrm_ctx_destroy(dlrm_ctx* ctx);
+int dlrm_ctx_set_stream(dlrm_ctx* ctx, void* stream);
+const char* dlrm_last_error(const dlrm_ctx* ctx);
+int dlrm_sync(dlrm_ctx* ctx);
+/* Synchronises, reads and clears the device out-of-range flag raised by any kernel since
+ * the previous call.  DLRM_E_INDEX if it was set. */
+int dlrm_check_bounds(dlrm_ctx* ctx);
+
+/* ---- device memory (so a host language without ROCm bindings can own buffers) ------- */
+int dlrm_malloc(dlrm_ctx* ctx, size_t bytes, void** dptr);
+int dlrm_free(dlrm_ctx* ctx, void* dptr);
+int dlrm_memcpy_h2d(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes); /* synchronous */
+int dlrm_memcpy_d2h(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes); /* synchronous */
+
+/* ---- embedding tables --------------------------------------------------------------- */
+/* Registers T tables of one dtype and feature size `dim` (SimpleEmbedding{Static{dim}}).
+ * data[t] points at a device [nrows[t]][dim] row-major table.  The table memory stays
+ * caller-owned; dlrm_sgd_update mutates it in place. */
+int dlrm_tables_create(dlrm_ctx* ctx, int num_tables, int dim, int dtype,
+                       void* const* data, const int64_t* nrows, dlrm_tables** out);
+int dlrm_tables_destroy(dlrm_tables* tables);
+
+/* maplookup(PreallocationStrategy(out_offset), tables, sparse):
+ *   out[b][out_offset + t*dim + c] = sum_{k<lookups} table_t[idx_t[b*lookups + k] - base][c]
+ * Columns [0, out_offset) are not touched (they are reserved for x, interact.jl:264-270).
+ * lookups = 1 is the one-hot copy (bit-exact); lookups > 1 sums in k order in fp32. */
+int dlrm_maplookup(dlrm_ctx* ctx, const dlrm_tables* tables,
+                   const void* indices, int itype, int64_t table_stride, int index_base,
+                   int batch, int lookups,
+                   void* out, int64_t out_ld, int64_t out_offset);
+
+/* ---- pairwise dot interaction -------------------------------------------------------- */
+/* (dot::DotInteraction)(x, ys): copies x[b][0:d] into ys[b][0:d] (fast_vcat), views
+ * ys[b][0:F*d] as T_b = [F][d], and writes
+ *   out[b] = [ x_b | Z[i][j] for i = 1..F-1, j = 0..i-1 | 0 * padding ],  Z = T_b T_b^T
+ * dtype applies to x, ys and out (bf16 in, fp32 accumulate, bf16 out). */
+int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch,
+                      const void* x, int64_t x_ld, void* ys, int64_t ys_ld,
+                      void* out, int64_t out_ld, int padding);
+
+/* dot_back(dot, dout, t, d, padding): S_b = symmetric zero-diagonal unpack of
+ * dout[b][d : d + F(F-1)/2];  dt[b] = S_b T_b  ([F][d], fp32, x-rows included as the
+ * reference returns them);  dx[b] = dout[b][0:d] + dt[b][0:d]  (fp32).
+ * t is the ys buffer of the forward pass (dtype as dout). */
+int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch,
+                      const void* dout, int64_t dout_ld, int padding,
+                      const void* t, int64_t t_ld,
+                      float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
+
+/* ---- sparse indexer + SGD scatter update --------------------------------------------- */
+int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_table,
+                        dlrm_indexer** out);
+int dlrm_indexer_destroy(dlrm_indexer* indexer);
+/* Dedupe: per table, a stable sort of positions by row -> unique rows + the positions that
+ * hit each of them in ascending order.  Asynchronous; device-side counts only. */
+int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
+                       const void* indices, int itype, int64_t table_stride, int index_base,
+                       int batch, int lookups);
+/* Inspection (synchronous): unique-row count of one table; if rows != NULL copies up to
+ * cap unique rows (0-based, ascending); if positions != NULL copies up to cap sorted
+ * positions (b*lookups + k) and their segment starts (cap+1 entries) into seg_start. */
+int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
+                      int64_t* num_unique, int64_t* rows, int64_t* positions,
+                      int64_t* seg_start, int64_t cap);
+
+/* update!(Descent(lr), tables, grads, indexers):
+ *   table_t[r] -= lr * sum_{(b,k): idx_t[b*lookups+k] - base == r} grad[b][grad_offset + t*dim + :]
+ * Default: deterministic (sum in ascending position order per unique row, one
+ * read-modify-write per unique row); builds the indexer from `indices` first unless
+ * DLRM_UPDATE_PREBUILT.  DLRM_UPDATE_ATOMIC ignores the indexer (may be NULL). */
+int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer, unsigned flags,
+                    const void* indices, int itype, int64_t table_stride, int index_base,
+                    int batch, int lookups,
+                    const void* grad, int grad_dtype, int64_t grad_ld, int64_t grad_offset,
+                    float lr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLRM_HIP_H */

@@ -1,0 +1,61 @@
+"""The C-ABI library: built, loadable, exporting exactly what include/dlrm_hip.h declares.
+CPU only — no compute call is made (no GPU here); only pure host entry points are called."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib(pkg):
+    return pkg._lib.load()
+
+
+def test_library_is_built_in_tree(pkg):
+    assert os.path.exists(pkg._lib.LIB_PATH), "run __graft_entry__.build()"
+    assert pkg._lib.LIB_PATH.startswith(ROOT)
+
+
+def test_every_header_symbol_is_exported_and_bound(pkg, lib):
+    names = pkg._lib.header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/dlrm_hip.h but not exported"
+        assert n in pkg._lib.SIGNATURES, f"{n} has no ctypes signature"
+    assert set(pkg._lib.SIGNATURES) == set(names)
+
+
+def test_ctypes_arity_matches_header(pkg):
+    text = open(pkg._lib.HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    for name, (_, args) in pkg._lib.SIGNATURES.items():
+        m = re.search(r"\b" + name + r"\s*\(([^)]*)\)", text)
+        assert m, name
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), (name, params, args)
+
+
+def test_abi_version(lib):
+    hdr = open(os.path.join(ROOT, "include", "dlrm_hip.h")).read()
+    v = int(re.search(r"#define DLRM_HIP_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.dlrm_abi_version() == v
+
+
+def test_null_arguments_are_rejected_without_touching_a_device(lib, pkg):
+    # argument validation happens on the host before any HIP call
+    assert lib.dlrm_ctx_create(0, None, None) == pkg._lib.E_ARG
+    assert lib.dlrm_maplookup(None, None, None, 0, 0, 0, 1, 1, None, 0, 0) == pkg._lib.E_ARG
+    assert lib.dlrm_interact_fwd(None, 0, 16, 2, 1, None, 16, None, 32, None, 17, 0) == pkg._lib.E_ARG
+    assert lib.dlrm_sgd_update(None, None, None, 0, None, 0, 0, 0, 1, 1, None, 0, 0, 0, 0.1) == pkg._lib.E_ARG
+    assert lib.dlrm_ctx_destroy(None) == 0
+    assert lib.dlrm_tables_destroy(None) == 0
+    assert lib.dlrm_indexer_destroy(None) == 0
+    assert lib.dlrm_last_error(None) == b"null context"
+
+
+def test_library_has_gfx950_code_object(pkg):
+    data = open(pkg._lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data

@@ -1,0 +1,369 @@
+"""GPU parity: the HIP path (through the C ABI) against the pinned CPU oracle and the goldens.
+
+Bars (see tests/helpers.py): bit-exact for one-hot lookups, pooled lookups (same fp32 add
+order as the oracle), unique rows and segment membership; fp32 tolerance for the MFMA
+interaction and chunked update sums; one bf16 rounding for bf16 outputs.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import assert_close, julia_isapprox, rand_indices, rand_tables
+
+pytestmark = pytest.mark.gpu
+
+
+def dev_tables(tables, device, dtype=torch.float32):
+    if dtype == torch.bfloat16:
+        return [torch.from_numpy(oracle.bf16_to_f32(oracle.f32_to_bf16(t))).to(device).to(torch.bfloat16)
+                for t in tables]
+    return [torch.from_numpy(t).to(device) for t in tables]
+
+
+def to_np_bits(t):
+    """device tensor -> numpy (bf16 as uint16 bit patterns, fp32 as float32)"""
+    t = t.detach().cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+def to_np_f32(t):
+    return t.detach().float().cpu().numpy()
+
+
+# ------------------------------------------------------------------ golden (HDF5) vectors
+@pytest.mark.parametrize("kind", ["single", "multi"])
+def test_golden_full_step(pkg, gpu, golden, kind):
+    """test/integration.jl + src/validation.jl on the GPU: lookup -> interaction -> backward ->
+    SGD(η=10), against the PyTorch goldens of the reference."""
+    g = golden[kind]
+    T, N, D = g["emb"].shape
+    B, d = g["mlp_bottom"].shape
+    L = int(g["L"])
+    tables = pkg.EmbeddingTableSet(dev_tables(list(g["emb"]), gpu))
+    idx = pkg.PackedIndices(torch.from_numpy(g["idx"]).reshape(T, B, L).to(gpu))
+    x = torch.from_numpy(g["mlp_bottom"]).to(gpu)
+    strategy = pkg.PreallocationStrategy(d)
+    ys = pkg.maplookup(strategy, tables, idx, index_base=0)
+    got = to_np_f32(ys[:, d:]).reshape(B, T, D)
+    if L == 1:
+        assert np.array_equal(got, g["concatenated"][:, 1:, :])
+    else:
+        assert_close(got, g["concatenated"][:, 1:, :], rtol=1e-6, what="pooled lookup vs PyTorch")
+        ref = np.zeros((B, d + T * D), dtype=np.float32)
+        oracle.maplookup(list(g["emb"]), g["idx"], 0, B, L, ref, d)
+        assert np.array_equal(got, ref[:, d:].reshape(B, T, D))  # same add order: bit-exact
+    dot = pkg.DotInteraction()
+    out, back = pkg.rrule(dot, x, ys)
+    o = to_np_f32(out)
+    assert np.array_equal(o[:, :d], g["mlp_bottom"])
+    assert_close(o[:, d:], g["zflat"], rtol=1e-5, what="zflat")
+    assert julia_isapprox(o, g["output_interaction"])
+    dout = torch.from_numpy(g["d_output_interaction"]).to(gpu)
+    _, dx, dy = back(dout)
+    grads = pkg.maplookup_pullback(d, tables, idx, dy)
+    pkg.update_(pkg.Descent(float(g["lr"])), tables, grads, index_base=0)
+    for t in range(T):
+        rows = g[f"upd_rows_{t}"]
+        new = to_np_f32(tables[t].data)
+        assert_close(new[rows], g[f"upd_vals_{t}"], rtol=1e-5, what=f"update_emb_{t}")
+        untouched = np.setdiff1d(np.arange(N), rows)
+        assert np.array_equal(new[untouched], g["emb"][t][untouched])
+
+
+# ------------------------------------------------------------------ lookup
+@pytest.mark.parametrize("dim", [4, 8, 16, 32, 64, 128, 256, 12])
+@pytest.mark.parametrize("lookups", [1, 3])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_lookup_vs_oracle(pkg, gpu, dim, lookups, dtype):
+    rng = np.random.default_rng(dim * 10 + lookups)
+    rows = [5, 1000, 3, 77]
+    B = 37
+    tabs = rand_tables(rng, rows, dim)
+    idx = rand_indices(rng, rows, B, lookups)
+    dt = dev_tables(tabs, gpu, dtype)
+    P = 8 if dtype == torch.bfloat16 else 4
+    out = pkg.maplookup(pkg.PreallocationStrategy(P), dt, torch.from_numpy(idx).reshape(len(rows), B, lookups).to(gpu),
+                        index_base=0)
+    ref_tabs = [to_np_bits(t) for t in dt]
+    ref = np.zeros((B, P + dim * len(rows)), dtype=ref_tabs[0].dtype)
+    oracle.maplookup(ref_tabs, idx, 0, B, lookups, ref, P)
+    assert np.array_equal(to_np_bits(out)[:, P:], ref[:, P:])
+
+
+@pytest.mark.parametrize("itype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("base", [0, 1])
+def test_lookup_index_types_and_base(pkg, gpu, itype, base):
+    rng = np.random.default_rng(3)
+    rows = [50, 60]
+    tabs = rand_tables(rng, rows, 16)
+    idx = rand_indices(rng, rows, 64, 2)
+    out = pkg.maplookup(pkg.PreallocationStrategy(0), dev_tables(tabs, gpu),
+                        torch.from_numpy(idx + base).to(itype).reshape(2, 64, 2).to(gpu), index_base=base)
+    ref = np.zeros((64, 32), dtype=np.float32)
+    oracle.maplookup(tabs, idx, 0, 64, 2, ref, 0)
+    assert np.array_equal(to_np_f32(out), ref)
+
+
+def test_lookup_default_strategy_and_lookup(pkg, gpu):
+    rng = np.random.default_rng(11)
+    tabs = rand_tables(rng, [9, 10], 8)
+    idx = [torch.tensor([1, 9, 3]), torch.tensor([10, 1, 1])]  # Julia 1-based
+    res = pkg.maplookup(pkg.DefaultStrategy(), dev_tables(tabs, gpu), idx)
+    assert np.array_equal(to_np_f32(res[0]), tabs[0][[0, 8, 2]])
+    assert np.array_equal(to_np_f32(res[1]), tabs[1][[9, 0, 0]])
+    one = pkg.lookup(dev_tables(tabs, gpu)[0], torch.tensor([2, 2]))
+    assert np.array_equal(to_np_f32(one), tabs[0][[1, 1]])
+
+
+def test_lookup_bounds_error(pkg, gpu):
+    tabs = dev_tables([np.ones((5, 16), dtype=np.float32)], gpu)
+    for bad in ([0, 6], [1, 7], [-3, 2]):
+        with pytest.raises(pkg.BoundsError):
+            pkg.maplookup(pkg.DefaultStrategy(), tabs, [torch.tensor(bad)])  # 1-based: 0, 6, 7, -3 invalid
+    # the error state is cleared after being reported
+    res = pkg.maplookup(pkg.DefaultStrategy(), tabs, [torch.tensor([1, 5])])
+    assert np.array_equal(to_np_f32(res[0]), np.ones((2, 16), dtype=np.float32))
+
+
+def test_lookup_empty_batch(pkg, gpu):
+    tabs = dev_tables([np.ones((5, 16), dtype=np.float32)], gpu)
+    out = pkg.maplookup(pkg.PreallocationStrategy(16), tabs, [torch.zeros(0, dtype=torch.int64)])
+    assert out.shape == (0, 32)
+
+
+# ------------------------------------------------------------------ interaction
+@pytest.mark.parametrize("d,F,B", [(16, 8, 128), (4, 4, 4), (128, 27, 300), (32, 17, 65), (64, 33, 20),
+                                   (16, 1, 5), (16, 2, 9), (8, 65, 7), (12, 5, 10), (128, 100, 3)])
+def test_interaction_fwd_bwd_vs_oracle(pkg, gpu, d, F, B):
+    rng = np.random.default_rng(d * 1000 + F)
+    x = rng.standard_normal((B, d)).astype(np.float32)
+    ys = np.zeros((B, F * d), dtype=np.float32)
+    ys[:, d:] = rng.standard_normal((B, (F - 1) * d)).astype(np.float32)
+    ref_ys = ys.copy()
+    ref = oracle.interact_fwd(x, ref_ys, F)
+    gys = torch.from_numpy(ys).to(gpu)
+    dot = pkg.DotInteraction()
+    out, back = pkg.rrule(dot, torch.from_numpy(x).to(gpu), gys)
+    assert np.array_equal(to_np_f32(gys), ref_ys)  # fast_vcat
+    o = to_np_f32(out)
+    assert np.array_equal(o[:, :d], x)
+    scale = float(np.abs(ys).max() ** 2 * d)
+    assert_close(o, ref, rtol=2e-6, scale=scale, what="interaction fwd")
+    dout = rng.standard_normal(ref.shape).astype(np.float32)
+    rdx, rdt = oracle.interact_bwd(dout, ref_ys, d, F)
+    _, dx, dt = back(torch.from_numpy(dout).to(gpu))
+    scale_b = float(np.abs(dout).max() * np.abs(ys).max() * F)
+    assert_close(to_np_f32(dt), rdt, rtol=2e-6, scale=scale_b, what="dt")
+    assert_close(to_np_f32(dx), rdx, rtol=2e-6, scale=scale_b, what="dx")
+
+
+@pytest.mark.parametrize("d,F,B", [(128, 27, 64), (16, 8, 33), (32, 17, 9)])
+def test_interaction_bf16(pkg, gpu, d, F, B):
+    rng = np.random.default_rng(5)
+    x = oracle.f32_to_bf16(rng.standard_normal((B, d)).astype(np.float32))
+    ys = oracle.f32_to_bf16(rng.standard_normal((B, F * d)).astype(np.float32))
+    ref_ys = ys.copy()
+    ref = oracle.interact_fwd(x, ref_ys, F)  # fp32 accumulate, one rounding
+    tx = torch.from_numpy(x.view(np.int16)).to(gpu).view(torch.bfloat16)
+    tys = torch.from_numpy(ys.view(np.int16)).to(gpu).view(torch.bfloat16)
+    out, back = pkg.rrule(pkg.DotInteraction(), tx, tys)
+    o = oracle.bf16_to_f32(to_np_bits(out))
+    r = oracle.bf16_to_f32(ref)
+    assert np.array_equal(to_np_bits(out)[:, :d], x)
+    assert_close(o, r, rtol=8e-3, scale=float(np.abs(r).max()), what="bf16 fwd")
+    dout = oracle.f32_to_bf16(rng.standard_normal(ref.shape).astype(np.float32))
+    rdx, rdt = oracle.interact_bwd(dout, ref_ys, d, F)
+    tdout = torch.from_numpy(dout.view(np.int16)).to(gpu).view(torch.bfloat16)
+    _, dx, dt = back(tdout)
+    assert dt.dtype == torch.float32 and dx.dtype == torch.float32  # dot_back returns fp32 (:419-424)
+    s = float(np.abs(rdt).max())
+    assert_close(to_np_f32(dt), rdt, rtol=2e-6, scale=s, what="bf16 dt")
+    assert_close(to_np_f32(dx), rdx, rtol=2e-6, scale=s, what="bf16 dx")
+
+
+def test_interaction_model_kat(pkg, gpu, kat):
+    m = kat["model"]
+    x = torch.tensor(m["bottom_mlp_output"], dtype=torch.float32, device=gpu)
+    tabs = [torch.tensor(t, dtype=torch.float32, device=gpu) for t in m["tables"]]
+    idx = [torch.tensor(i) + 1 for i in m["sparse_idx0"]]  # model.jl:117 adds 1
+    ys = pkg.maplookup(pkg.PreallocationStrategy(4), tabs, idx)
+    for t in range(3):
+        np.testing.assert_allclose(to_np_f32(ys[:, 4 + 4 * t:8 + 4 * t]), np.array(m["embedding_outputs"][t]), atol=1e-6)
+    out = pkg.DotInteraction()(x, ys)
+    np.testing.assert_allclose(to_np_f32(out), np.array(m["interaction_output"]), atol=1e-4)
+
+
+# ------------------------------------------------------------------ indexer + update
+def _np_segments(idx_row):
+    rows = np.unique(idx_row)
+    order = np.argsort(idx_row, kind="stable")
+    return rows, order
+
+
+@pytest.mark.parametrize("rows,B,L", [([3, 4, 10, 1000, 5_000_000], 2048, 1), ([1000, 7, 20000], 300, 10),
+                                      ([2], 1, 1), ([100000, 3], 5000, 1)])
+def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L):
+    rng = np.random.default_rng(B + L)
+    idx = rand_indices(rng, rows, B, L)
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B * L, gpu)
+    ix.build(tabs, torch.from_numpy(idx).reshape(len(rows), B, L).to(gpu), index_base=0)
+    for t in range(len(rows)):
+        urows, order = _np_segments(idx[t])
+        got_rows, pos, seg = ix.segments(t)
+        assert got_rows == urows.tolist()
+        assert pos == order.tolist()  # stable: ascending positions within each row
+        assert seg[-1] == B * L and len(seg) == len(urows) + 1
+
+
+@pytest.mark.parametrize("dim", [16, 128, 256, 8, 12])
+@pytest.mark.parametrize("L", [1, 4])
+def test_sgd_update_vs_oracle(pkg, gpu, dim, L):
+    rng = np.random.default_rng(dim + 100 * L)
+    rows = [3, 4, 27, 1000, 200000]
+    B = 1024
+    tabs = rand_tables(rng, rows, dim)
+    idx = rand_indices(rng, rows, B, L)
+    Pd = 16
+    grad = rng.standard_normal((B, Pd + dim * len(rows))).astype(np.float32)
+    ref = [t.copy() for t in tabs]
+    uniq = oracle.sgd_update(ref, idx, 0, B, L, grad, Pd, 0.5)
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    pidx = pkg.PackedIndices(torch.from_numpy(idx).reshape(len(rows), B, L).to(gpu))
+    grads = pkg.maplookup_pullback(Pd, ts, pidx, torch.from_numpy(grad).to(gpu))
+    ix = pkg.SparseIndexer(len(rows), B * L, gpu)
+    pkg.update_(pkg.Descent(0.5), ts, grads, ix, index_base=0)
+    for t in range(len(rows)):
+        assert len(ix.unique_rows(t)) == uniq[t]
+        new = to_np_f32(ts[t].data)
+        touched = np.unique(idx[t])
+        # hot rows (3-row table: ~340 hits each) are summed in 32-position chunks: tolerance
+        scale = 0.5 * np.abs(grad).max() * B * L
+        assert_close(new[touched], ref[t][touched], rtol=1e-6, scale=scale, what=f"table {t}")
+        untouched = np.setdiff1d(np.arange(rows[t]), touched)
+        assert np.array_equal(new[untouched], tabs[t][untouched])
+
+
+def test_sgd_update_bitwise_deterministic_and_atomic_close(pkg, gpu):
+    rng = np.random.default_rng(99)
+    rows = [3, 10, 100000]
+    B, D = 4096, 128
+    tabs = rand_tables(rng, rows, D)
+    idx = torch.from_numpy(rand_indices(rng, rows, B, 1)).to(gpu)
+    grad = torch.from_numpy(rng.standard_normal((B, D * len(rows))).astype(np.float32)).to(gpu)
+    results = []
+    for mode in ("det", "det", "atomic"):
+        ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+        p = pkg.PackedIndices(idx)
+        grads = pkg.maplookup_pullback(0, ts, p, grad)
+        pkg.update_(pkg.Descent(0.1), ts, grads, index_base=0, deterministic=(mode == "det"))
+        results.append([to_np_f32(t.data) for t in ts])
+    for a, b in zip(results[0], results[1]):
+        assert np.array_equal(a, b)  # bitwise reproducible
+    for a, c in zip(results[0], results[2]):
+        assert_close(c, a, rtol=1e-6, scale=0.1 * 4.0 * B, what="atomic vs deterministic")
+
+
+def test_sgd_update_integer_gradients_exact(pkg, gpu):
+    """Exactly representable sums: order cannot matter, so GPU == closed form bit for bit."""
+    rng = np.random.default_rng(5)
+    rows = [3, 50, 10000]
+    B, D, L = 2048, 32, 2
+    tabs = [np.zeros((n, D), dtype=np.float32) for n in rows]
+    idx = rand_indices(rng, rows, B, L)
+    grad = rng.integers(-8, 8, size=(B, D * len(rows))).astype(np.float32)
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    p = pkg.PackedIndices(torch.from_numpy(idx).reshape(3, B, L).to(gpu))
+    pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, torch.from_numpy(grad).to(gpu)), index_base=0)
+    for t, n in enumerate(rows):
+        want = np.zeros((n, D))
+        np.add.at(want, idx[t], np.repeat(grad[:, t * D:(t + 1) * D], L, axis=0))
+        assert np.array_equal(to_np_f32(ts[t].data), (-want).astype(np.float32))
+
+
+def test_update_bounds_error(pkg, gpu):
+    ts = pkg.EmbeddingTableSet([torch.zeros((4, 16), device=gpu)])
+    p = pkg.PackedIndices([torch.tensor([1, 5])])
+    g = torch.ones((2, 16), device=gpu)
+    with pytest.raises(pkg.BoundsError):
+        pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, g))
+    # the valid index was still applied, the invalid one skipped
+    assert to_np_f32(ts[0].data)[0].tolist() == [-1.0] * 16
+
+
+# ------------------------------------------------------------------ the engine
+@pytest.mark.parametrize("overlap", [False, True])
+def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap):
+    rng = np.random.default_rng(1)
+    rows = [10, 3000, 7, 100000]
+    D, B = 32, 512
+    tabs = rand_tables(rng, rows, D)
+    idx = torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = len(rows) + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0,
+                     overlap_indexer=overlap)
+    p = pkg.PackedIndices(idx)
+    hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    # same thing through the reference-shaped operator API
+    ts2 = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts2, p, index_base=0)
+    out, back = pkg.rrule(pkg.DotInteraction(), x, ys)
+    _, dx, dy = back(dout)
+    pkg.update_(pkg.Descent(0.25), ts2, pkg.maplookup_pullback(D, ts2, p, dy), index_base=0)
+    assert np.array_equal(to_np_f32(hp.out), to_np_f32(out))
+    assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
+    for a, b in zip(hp.ts, ts2):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_full_size_properties_metric_config(pkg, gpu):
+    """BASELINE metric shape (26 Kaggle tables x 128 fp32, B=2048): properties that need no
+    CPU oracle at 17 GB — row-encoded gather exactness, the interaction adjoint identity
+    <dz, tri(T T')> == 1/2 <dT, T>, and an exact integer-gradient update."""
+    rows = pkg.KAGGLE_EMBEDDING_SIZES
+    D, B = 128, 2048
+    T = len(rows)
+    g = torch.Generator(device=gpu).manual_seed(0)
+    # encode (table, row) into every element exactly: value = row mod 4093 + 4096 * t + c/128
+    tabs = []
+    for t, n in enumerate(rows):
+        r = torch.arange(n, device=gpu, dtype=torch.float32).remainder_(4093).add_(4096.0 * t)
+        tabs.append((r[:, None] + torch.arange(D, device=gpu, dtype=torch.float32)[None, :] / 128.0).contiguous())
+    ts = pkg.EmbeddingTableSet(tabs)
+    idx = torch.stack([torch.randint(0, n, (B,), device=gpu, generator=g) for n in rows]).to(torch.int32)
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, pkg.PackedIndices(idx), index_base=0)
+    want = (idx.to(torch.float32).T.remainder(4093) + 4096.0 * torch.arange(T, device=gpu)[None, :])
+    want = want[:, :, None] + torch.arange(D, device=gpu, dtype=torch.float32)[None, None, :] / 128.0
+    assert torch.equal(ys[:, D:].reshape(B, T, D), want)
+    # interaction adjoint identity on random data
+    x = torch.randn((B, D), device=gpu, generator=g)
+    ys2 = torch.randn((B, (T + 1) * D), device=gpu, generator=g) * 0.1
+    out, back = pkg.rrule(pkg.DotInteraction(), x, ys2)
+    dz = torch.randn(out.shape, device=gpu, generator=g)
+    dz[:, :D] = 0
+    _, dx, dt = back(dz)
+    lhs = (dz[:, D:].double() * out[:, D:].double()).sum()
+    rhs = 0.5 * (dt.double() * ys2.double()).sum()
+    assert abs(lhs - rhs) <= 1e-5 * (dz.abs().double() * out.abs().double()).sum()
+    # torch fp32 reference of the interaction at full size
+    Tm = ys2.reshape(B, T + 1, D).double()
+    Z = Tm @ Tm.transpose(1, 2)
+    li, lj = torch.tril_indices(T + 1, T + 1, -1, device=gpu)
+    assert torch.allclose(out[:, D:].double(), Z[:, li, lj], rtol=1e-5, atol=1e-5)
+    # exact update with integer gradients on zeroed tables
+    zt = pkg.EmbeddingTableSet([torch.zeros((n, D), device=gpu) for n in rows])
+    gi = torch.randint(-4, 5, (B, D * T), device=gpu, generator=g).to(torch.float32)
+    pidx = pkg.PackedIndices(idx)
+    pkg.update_(pkg.Descent(1.0), zt, pkg.maplookup_pullback(0, zt, pidx, gi), index_base=0)
+    for t in (0, 8, 2, 25):  # a 1460-row, a 3-row, a 10M-row and the last table
+        ref = torch.zeros((rows[t], D), device=gpu, dtype=torch.float64)
+        ref.index_add_(0, idx[t].long(), gi[:, t * D:(t + 1) * D].double())
+        assert torch.equal(zt[t].data, (-ref).float())
