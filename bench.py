@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
     ap.add_argument("--overlap-indexer", type=int, default=1)
+    ap.add_argument("--fused", type=int, default=1)
     return ap.parse_args()
 
 
@@ -50,6 +51,8 @@ def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks):
     P = F * (F - 1) // 2
     N = B * L
     return {
+        # fused maplookup + interaction: x, L rows + L indices per table in; ys (x + T rows) and out written
+        "lookup_interact_fwd": B * (d * E + T * L * (I + D * E) + F * D * E + (d + P) * E),
         "lookup": T * B * (L * I + L * D * E + D * E),
         "interact_fwd": B * (d * E + (F - 1) * D * E + d * E + (d + P) * E),
         "interact_bwd": B * ((d + P) * E + F * D * E + F * D * 4 + d * 4),
@@ -151,12 +154,15 @@ def main():
     if world == 1:
         tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows)
         ts = pkg.EmbeddingTableSet(tables)
-        engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0, overlap_indexer=bool(a.overlap_indexer))
+        engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0, overlap_indexer=bool(a.overlap_indexer),
+                             fused=bool(a.fused))
         F = T + 1
         dtp = tables[0].dtype
         x = torch.randn((B, D), device=dev, generator=g).to(dtp)
         dout = (torch.randn((B, engine.width), device=dev, generator=g) * 1e-3).to(dtp)
         packs = [pkg.PackedIndices(i.reshape(T, B, L)) for i in idx]
+        for p in packs:
+            engine.validate(x, p, dout)
 
         def step(k):
             engine.step(x, packs[k % NBATCH], dout)
@@ -222,29 +228,28 @@ def main():
         uniq = chunks = 0
         for k in range(NBATCH):
             engine.build_indexer(packs[k])
-            cnt = np.zeros(8, dtype=np.int32)
             torch.cuda.synchronize()
             for t in range(T):
                 uniq += len(engine.indexer.unique_rows(t))
         uniq /= NBATCH
         chunks = uniq  # one chunk per unique row, plus a few for hot rows
         bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks)
-        names = ["lookup", "interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
+        if engine.fused:
+            names = ["lookup_interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
+            fns = [lambda p: engine.lookup_interact_fwd(x, p), engine.build_indexer,
+                   lambda p: engine.interact_bwd(dout), lambda p: engine.sgd_update(p, prebuilt=True)]
+        else:
+            names = ["lookup", "interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
+            fns = [engine.lookup, lambda p: engine.interact_fwd(x), engine.build_indexer,
+                   lambda p: engine.interact_bwd(dout), lambda p: engine.sgd_update(p, prebuilt=True)]
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(a.steps)]
         for k in range(a.steps):
             p = packs[k % NBATCH]
             e = evs[k]
             e[0].record()
-            engine.lookup(p)
-            e[1].record()
-            engine.interact_fwd(x)
-            e[2].record()
-            engine.build_indexer(p)
-            e[3].record()
-            engine.interact_bwd(dout)
-            e[4].record()
-            engine.sgd_update(p, prebuilt=True)
-            e[5].record()
+            for i, fn in enumerate(fns):
+                fn(p)
+                e[i + 1].record()
         torch.cuda.synchronize()
         stages = {}
         for i, n in enumerate(names):

@@ -243,6 +243,26 @@ int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
     return launch_interact_fwd(ctx, dtype, d, num_features, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
 }
 
+int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
+                             int64_t table_stride, int index_base, int batch, int lookups, const void* x,
+                             int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {
+    CHECK_ARG(ctx && tb, "dlrm_lookup_interact_fwd: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    const int d = tb->D, F = tb->T + 1;
+    const int64_t P = (int64_t)F * (F - 1) / 2;
+    CHECK_ARG(padding >= 0 && x_ld >= d && ys_ld >= (int64_t)F * d && out_ld >= d + P + padding,
+              "dlrm_lookup_interact_fwd: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (x && ys && out), "dlrm_lookup_interact_fwd: null buffer");
+    rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                    index_base, lookups, d, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
+    if (rc != DLRM_E_UNSUPPORTED) return rc;
+    rc = launch_maplookup(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype, table_stride,
+                          index_base, batch, lookups, ys, ys_ld, d);
+    if (rc) return rc;
+    return launch_interact_fwd(ctx, tb->dtype, d, F, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
+}
+
 int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* dout, int64_t dout_ld,
                       int padding, const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
     CHECK_ARG(ctx, "dlrm_interact_bwd: null ctx");
@@ -277,8 +297,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     Piece pieces[] = {
         {(void**)&ix->dev.keys0, n * 4},     {(void**)&ix->dev.keys1, n * 4},   {(void**)&ix->dev.vals0, n * 4},
         {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
-        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.ch_beg, n * 4},  {(void**)&ix->dev.ch_end, n * 4},
-        {(void**)&ix->dev.ch_row, n * 4},    {(void**)&ix->dev.ch_slot, n * 4}, {(void**)&ix->dev.hot_row, n * 4},
+        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot_row, n * 4},
         {(void**)&ix->dev.hot_slot0, n * 4}, {(void**)&ix->dev.hot_n, n * 4},  {(void**)&ix->dev.counts, (size_t)T * 32},
     };
     size_t total = 0;

@@ -78,7 +78,7 @@ struct IndexerDev {
     int32_t* perm;         // sorted positions (valid prefix)
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
-    int32_t* ch_beg;  int32_t* ch_end;  uint32_t* ch_row;  int32_t* ch_slot;
+    int4* chunks;          // {beg, end, row, slot}: slot < 0 = single-chunk segment
     uint32_t* hot_row; int32_t* hot_slot0; int32_t* hot_n;
     int32_t* counts;       // [T][8]: U, chunks, hot, hot_chunks, nvalid
     int64_t cap;
@@ -101,6 +101,10 @@ int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16
                      int64_t out_ld, int64_t out_off);
 int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
                         int64_t ys_ld, void* out, int64_t out_ld, int padding);
+int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
+                               const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                               const void* x, int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld,
+                               int padding);
 int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,

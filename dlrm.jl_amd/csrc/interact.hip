@@ -38,36 +38,75 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Writes one packed element (index e of the sample's output row).
-template <typename T>
-__device__ __forceinline__ void put_out(float* stage, bool staged, T* orow, int e, float v) {
-    if (staged) stage[e] = v;
-    else orow[e] = from_f32<T>(v);
-}
-
-template <typename T, int NB>
-__device__ __forceinline__ void scatter_pairs(const f32x4_t (&acc)[NB * (NB + 1) / 2], int F, int d, int lane,
-                                              float* stage, bool staged, T* orow) {
-    const int c = lane & 15, q = lane >> 4;
-    int ij = 0;
-#pragma unroll
-    for (int I = 0; I < NB; ++I)
-#pragma unroll
-        for (int J = 0; J <= I; ++J, ++ij) {
-            const int j = J * 16 + c;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = I * 16 + 4 * q + r;
-                if (i < F && j < i) put_out<T>(stage, staged, orow, d + i * (i - 1) / 2 + j, acc[ij][r]);
-            }
-        }
-}
-
 // ---------------------------------------------------------------------------------- fwd
-template <int NB>
-__global__ __launch_bounds__(256) void interact_fwd_f32(int d, int F, int B, const float* __restrict__ x,
-                                                        int64_t x_ld, float* __restrict__ ys, int64_t ys_ld,
-                                                        float* __restrict__ out, int64_t out_ld, int padding) {
+// Fragment traits: fp32 -> v_mfma_f32_16x16x4_f32 with float4 loads (16 columns per step, 4
+// MFMA k-steps, one per component); bf16 -> v_mfma_f32_16x16x32_bf16 with 8-element loads
+// (32 columns per step, one MFMA).
+template <typename T> struct Frag;
+template <> struct Frag<float> {
+    typedef f32x4_t type;
+    static constexpr int COLS = 16, PER_LANE = 4;
+    __device__ static inline type zero() { return type{0.f, 0.f, 0.f, 0.f}; }
+    __device__ static inline void mma(f32x4_t& acc, const type& a, const type& b) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], b[k], acc, 0, 0, 0);
+    }
+    __device__ static inline void add_to(float* f, const type& v) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) f[k] += v[k];
+    }
+    __device__ static inline void to_f(float* f, const type& v) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) f[k] = v[k];
+    }
+    __device__ static inline type from_f(const float* f) { return type{f[0], f[1], f[2], f[3]}; }
+};
+template <> struct Frag<uint16_t> {
+    typedef bf16x8_t type;
+    static constexpr int COLS = 32, PER_LANE = 8;
+    __device__ static inline type zero() { return type{}; }
+    __device__ static inline void mma(f32x4_t& acc, const type& a, const type& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+    __device__ static inline void to_f(float* f, const type& v) {
+        const u16x8 u = __builtin_bit_cast(u16x8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = bf16_to_f32(u[k]);
+    }
+    __device__ static inline void add_to(float* f, const type& v) {
+        float g[8];
+        to_f(g, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += g[k];
+    }
+    __device__ static inline type from_f(const float* f) {
+        u16x8 u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[k] = f32_to_bf16(f[k]);
+        return __builtin_bit_cast(type, u);
+    }
+};
+
+// Where the embedding rows come from: the ys buffer (the reference's two-operator form), or
+// straight from the tables (maplookup fused into the interaction: every gathered row is read
+// once into MFMA fragments and written to ys from registers — ys is never read back).
+struct GatherArgs {
+    const TableDesc* tabs;
+    const void* idx;
+    int itype;
+    int64_t tstride;
+    int base;
+    int L;
+    unsigned* err;
+};
+
+template <typename T, int NB, bool FUSED>
+__global__ __launch_bounds__(256) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x, int64_t x_ld,
+                                                           T* __restrict__ ys, int64_t ys_ld, T* __restrict__ out,
+                                                           int64_t out_ld, int padding, GatherArgs ga) {
+    typedef Frag<T> FR;
+    typedef typename FR::type frag;
+    constexpr int UU = 4;  // column steps whose loads are issued together
     __shared__ float stage_all[4][kStage];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
@@ -76,120 +115,121 @@ __global__ __launch_bounds__(256) void interact_fwd_f32(int d, int F, int B, con
     const bool staged = W <= kStage;
     float* stage = stage_all[w];
     for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < B; b += (int64_t)gridDim.x * 4) {
-        const float* xb = x + b * x_ld;
-        float* yb = ys + b * ys_ld;
-        float* orow = out + b * out_ld;
+        const T* xb = x + b * x_ld;
+        T* yb = ys + b * ys_ld;
+        T* orow = out + b * out_ld;
         // fast_vcat: x into the reserved rows of ys; x is also the head of the output row.
         for (int i = lane; i < d; i += 64) {
-            const float v = xb[i];
+            const T v = xb[i];
             yb[i] = v;
-            put_out<float>(stage, staged, orow, i, v);
+            if (staged) stage[i] = to_f32(v);
+            else orow[i] = v;
+        }
+        // row sources: feature 0 is x itself; features 1..F-1 are ys rows or table rows
+        const T* src[NB];
+        int64_t kidx[NB];  // FUSED, pooled: index position of lookup 0 of this (table, sample)
+#pragma unroll
+        for (int I = 0; I < NB; ++I) {
+            const int row = I * 16 + c;
+            src[I] = nullptr;
+            kidx[I] = -1;
+            if (row == 0) {
+                src[I] = xb;
+            } else if (row < F) {
+                if (!FUSED) {
+                    src[I] = yb + (int64_t)row * d;
+                } else {
+                    const int t = row - 1;
+                    kidx[I] = t * ga.tstride + b * ga.L;
+                    const int64_t r = load_index(ga.idx, ga.itype, kidx[I]) - ga.base;
+                    if (r >= 0 && r < ga.tabs[t].nrows) src[I] = (const T*)ga.tabs[t].data + r * d;
+                    else if (q == 0) raise_index_error(ga.err);
+                }
+            }
         }
         f32x4_t acc[NB * (NB + 1) / 2];
 #pragma unroll
         for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        // feature 0 is read from x itself (ys rows 0..d-1 were just written by this wave)
-        const float* rowp[NB];
+        for (int u0 = 0; u0 < d; u0 += UU * FR::COLS) {
+            frag a[UU][NB];
 #pragma unroll
-        for (int I = 0; I < NB; ++I) {
-            const int row = I * 16 + c;
-            rowp[I] = row >= F ? nullptr : (row == 0 ? xb : yb + (int64_t)row * d);
-        }
-        for (int u = 0; u < d; u += 16) {
-            const int col = u + 4 * q;
-            f32x4_t a[NB];
+            for (int uu = 0; uu < UU; ++uu) {
+                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
 #pragma unroll
-            for (int I = 0; I < NB; ++I)
-                a[I] = (rowp[I] && col < d) ? *(const f32x4_t*)(rowp[I] + col) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+                for (int I = 0; I < NB; ++I)
+                    a[uu][I] = (src[I] && col < d) ? *(const frag*)(src[I] + col) : FR::zero();
+            }
+            if (FUSED) {
+                // pooled bags: add lookups 1..L-1 in k order (fp32), round once to T
+                if (ga.L > 1) {
 #pragma unroll
-            for (int comp = 0; comp < 4; ++comp) {
+                    for (int I = 0; I < NB; ++I) {
+                        if (kidx[I] < 0) continue;
+                        const int t = I * 16 + c - 1;
+                        float f[UU][FR::PER_LANE];
+#pragma unroll
+                        for (int uu = 0; uu < UU; ++uu) FR::to_f(f[uu], a[uu][I]);
+                        for (int k = 1; k < ga.L; ++k) {
+                            const int64_t r = load_index(ga.idx, ga.itype, kidx[I] + k) - ga.base;
+                            const T* rp = nullptr;
+                            if (r >= 0 && r < ga.tabs[t].nrows) rp = (const T*)ga.tabs[t].data + r * d;
+                            else if (q == 0 && u0 == 0) raise_index_error(ga.err);
+#pragma unroll
+                            for (int uu = 0; uu < UU; ++uu) {
+                                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
+                                if (rp && col < d) FR::add_to(f[uu], *(const frag*)(rp + col));
+                            }
+                        }
+#pragma unroll
+                        for (int uu = 0; uu < UU; ++uu) a[uu][I] = FR::from_f(f[uu]);
+                    }
+                }
+                // the lookup output: ys rows 1..F-1 written from the fragments
+#pragma unroll
+                for (int uu = 0; uu < UU; ++uu) {
+                    const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) {
+                        const int row = I * 16 + c;
+                        if (row >= 1 && row < F && col < d) *(frag*)(yb + (int64_t)row * d + col) = a[uu][I];
+                    }
+                }
+            }
+#pragma unroll
+            for (int uu = 0; uu < UU; ++uu) {
                 int ij = 0;
 #pragma unroll
                 for (int I = 0; I < NB; ++I)
 #pragma unroll
-                    for (int J = 0; J <= I; ++J, ++ij)
-                        acc[ij] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[I][comp], a[J][comp], acc[ij], 0, 0, 0);
+                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[ij], a[uu][I], a[uu][J]);
             }
         }
-        scatter_pairs<float, NB>(acc, F, d, lane, stage, staged, orow);
-        for (int e = d + P + lane; e < W; e += 64) put_out<float>(stage, staged, orow, e, 0.0f);
-        if (staged) {
-            wave_lds_sync();
-            for (int e = lane; e < W; e += 64) orow[e] = stage[e];
-            wave_lds_sync();
-        }
-    }
-}
-
-template <int NB>
-__global__ __launch_bounds__(256) void interact_fwd_bf16(int d, int F, int B, const uint16_t* __restrict__ x,
-                                                         int64_t x_ld, uint16_t* __restrict__ ys, int64_t ys_ld,
-                                                         uint16_t* __restrict__ out, int64_t out_ld, int padding) {
-    __shared__ float stage_all[4][kStage];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 15, q = lane >> 4;
-    const int P = F * (F - 1) / 2;
-    const int W = d + P + padding;
-    const bool staged = W <= kStage;
-    float* stage = stage_all[w];
-    for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < B; b += (int64_t)gridDim.x * 4) {
-        const uint16_t* xb = x + b * x_ld;
-        uint16_t* yb = ys + b * ys_ld;
-        uint16_t* orow = out + b * out_ld;
-        for (int i = lane; i < d; i += 64) {
-            const uint16_t v = xb[i];
-            yb[i] = v;
-            if (staged) stage[i] = bf16_to_f32(v);
-            else orow[i] = v;
-        }
-        f32x4_t acc[NB * (NB + 1) / 2];
-#pragma unroll
-        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const uint16_t* rowp[NB];
-#pragma unroll
-        for (int I = 0; I < NB; ++I) {
-            const int row = I * 16 + c;
-            rowp[I] = row >= F ? nullptr : (row == 0 ? xb : yb + (int64_t)row * d);
-        }
-        for (int u = 0; u < d; u += 32) {
-            const int col = u + 8 * q;
-            bf16x8_t a[NB];
-#pragma unroll
-            for (int I = 0; I < NB; ++I) {
-                if (rowp[I] && col < d) a[I] = *(const bf16x8_t*)(rowp[I] + col);
-                else a[I] = bf16x8_t{};
-            }
+        // Z[i][j], i > j: triangular_slice_kernel! order (i-major), after x
+        {
             int ij = 0;
 #pragma unroll
             for (int I = 0; I < NB; ++I)
 #pragma unroll
-                for (int J = 0; J <= I; ++J, ++ij)
-                    acc[ij] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[I], a[J], acc[ij], 0, 0, 0);
-        }
-        // stage holds fp32 values; the final store rounds once to bf16
-        int ij = 0;
+                for (int J = 0; J <= I; ++J, ++ij) {
+                    const int j = J * 16 + c;
 #pragma unroll
-        for (int I = 0; I < NB; ++I)
-#pragma unroll
-            for (int J = 0; J <= I; ++J, ++ij) {
-                const int j = J * 16 + c;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = I * 16 + 4 * q + r;
-                    if (i < F && j < i) {
-                        const int e = d + i * (i - 1) / 2 + j;
-                        if (staged) stage[e] = acc[ij][r];
-                        else orow[e] = f32_to_bf16(acc[ij][r]);
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = I * 16 + 4 * q + r;
+                        if (i < F && j < i) {
+                            const int e = d + i * (i - 1) / 2 + j;
+                            if (staged) stage[e] = acc[ij][r];
+                            else orow[e] = from_f32<T>(acc[ij][r]);
+                        }
                     }
                 }
-            }
+        }
         for (int e = d + P + lane; e < W; e += 64) {
             if (staged) stage[e] = 0.0f;
-            else orow[e] = 0;
+            else orow[e] = from_f32<T>(0.0f);
         }
         if (staged) {
             wave_lds_sync();
-            for (int e = lane; e < W; e += 64) orow[e] = f32_to_bf16(stage[e]);
+            for (int e = lane; e < W; e += 64) orow[e] = from_f32<T>(stage[e]);
             wave_lds_sync();
         }
     }
@@ -203,12 +243,26 @@ template <int NB> struct BwdGeom {
     static constexpr int LDS_FLOATS = NS * SS;                  // per wave
 };
 
+// 4 consecutive elements of T as fp32 (16-B load for fp32, 8-B for bf16)
+__device__ __forceinline__ f32x4_t load4_f32(const float* p) { return *(const f32x4_t*)p; }
+__device__ __forceinline__ f32x4_t load4_f32(const uint16_t* p) {
+    const uint2 v = *(const uint2*)p;
+    return f32x4_t{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                   __uint_as_float(v.y & 0xffff0000u)};
+}
+
+// dT = S T per sample, in 64-column super-blocks: lane (c, q) loads T[4s+q][64sb+4c .. +3]
+// (16 lanes read 256 contiguous bytes of a row), and component e of that float4 is the B
+// operand of the MFMA that produces output columns 64sb + 4j + e.  The four accumulators of
+// a tile row then hold 4 consecutive output columns per lane -> one float4 store per row.
+// All k-step loads of a super-block are issued before its MFMAs (up to 4*NB in flight).
 template <typename T, int NB>
 __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
                                                            int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
                                                            float* __restrict__ dx, int64_t dx_ld,
                                                            float* __restrict__ dt, int64_t dt_ld) {
     typedef BwdGeom<NB> G;
+    constexpr int KS = 4 * NB;  // max k-steps (F <= 16 NB)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (w >= G::WPB) return;
@@ -232,29 +286,47 @@ __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, 
             S[j * G::SS + i] = v;
         }
         wave_lds_sync();
-        for (int nb = 0; nb < d; nb += 16) {
-            const int n = nb + c;
-            f32x4_t acc[NB];
+        for (int sb = 0; sb < d; sb += 64) {
+            const int n0 = sb + 4 * c;  // this lane's 4 output columns
+            const bool colok = n0 < d;
+            f32x4_t bv[KS];
 #pragma unroll
-            for (int I = 0; I < NB; ++I) acc[I] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            for (int s = 0; s < ksteps; ++s) {
+            for (int s = 0; s < KS; ++s) {
                 const int kk = 4 * s + q;
-                const float bv = (kk < F && n < d) ? to_f32(tb[(int64_t)kk * d + n]) : 0.0f;
+                bv[s] = (s < ksteps && kk < F && colok) ? load4_f32(tb + (int64_t)kk * d + n0)
+                                                        : f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+            f32x4_t acc[NB][4];
 #pragma unroll
-                for (int I = 0; I < NB; ++I) {
-                    const float av = S[kk * G::SS + I * 16 + c];  // = S[16I+c][kk] (symmetric)
-                    acc[I] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[I], 0, 0, 0);
+            for (int I = 0; I < NB; ++I)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                if (s < ksteps) {
+                    const int kk = 4 * s + q;
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) {
+                        const float av = S[kk * G::SS + I * 16 + c];  // = S[16I+c][kk] (symmetric)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s][e], acc[I][e], 0, 0, 0);
+                    }
                 }
             }
-            if (n < d) {
+            if (colok) {
 #pragma unroll
                 for (int I = 0; I < NB; ++I)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int f = I * 16 + 4 * q + r;
                         if (f < F) {
-                            dt[b * dt_ld + (int64_t)f * d + n] = acc[I][r];
-                            if (f == 0) dx[b * dx_ld + n] = to_f32(ob[n]) + acc[I][r];
+                            const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
+                            *(f32x4_t*)(dt + b * dt_ld + (int64_t)f * d + n0) = v;
+                            if (f == 0) {
+                                const f32x4_t xo = load4_f32(ob + n0);
+                                *(f32x4_t*)(dx + b * dx_ld + n0) = xo + v;
+                            }
                         }
                     }
             }
@@ -324,16 +396,24 @@ static unsigned grid_for(int64_t items, int per_block, int cus) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
-template <int NB>
-static void launch_fwd_nb(hipStream_t s, int cus, int dtype, int d, int F, int B, const void* x, int64_t x_ld,
-                          void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {
+template <typename T, int NB, bool FUSED>
+static void launch_fwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
+                          int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
     const unsigned g = grid_for(B, 4, cus);
-    if (dtype == DLRM_F32)
-        hipLaunchKernelGGL(interact_fwd_f32<NB>, dim3(g), dim3(256), 0, s, d, F, B, (const float*)x, x_ld,
-                           (float*)ys, ys_ld, (float*)out, out_ld, padding);
-    else
-        hipLaunchKernelGGL(interact_fwd_bf16<NB>, dim3(g), dim3(256), 0, s, d, F, B, (const uint16_t*)x, x_ld,
-                           (uint16_t*)ys, ys_ld, (uint16_t*)out, out_ld, padding);
+    hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x, x_ld,
+                       (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+}
+
+template <typename T, bool FUSED>
+static bool dispatch_fwd(int NB, hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
+                         int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
+    switch (NB) {
+#define DLRM_CASE(N) \
+    case N: launch_fwd_nb<T, N, FUSED>(s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga); return true;
+        DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(3) DLRM_CASE(4) DLRM_CASE(5) DLRM_CASE(6)
+#undef DLRM_CASE
+        default: return false;
+    }
 }
 
 template <typename T, int NB>
@@ -346,26 +426,25 @@ static void launch_bwd_nb(hipStream_t s, int cus, int d, int F, int B, const voi
                        dout_ld, (const T*)t, t_ld, dx, dx_ld, dt, dt_ld);
 }
 
+static bool fwd_aligned(int dtype, int d, const void* x, int64_t x_ld, const void* ys, int64_t ys_ld) {
+    const int vec = dtype == DLRM_F32 ? 4 : 8;  // elements per 16-B fragment load
+    return (uintptr_t)x % 16 == 0 && (uintptr_t)ys % 16 == 0 && (x_ld % vec) == 0 && (ys_ld % vec) == 0 &&
+           (d % vec) == 0;
+}
+
 int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
                         int64_t ys_ld, void* out, int64_t out_ld, int padding) {
     if (B == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
-    const int esz = dtype == DLRM_F32 ? 4 : 2;
-    const int vec = 16 / esz;
-    const bool aligned = (uintptr_t)x % 16 == 0 && (uintptr_t)ys % 16 == 0 && (x_ld % vec) == 0 &&
-                         (ys_ld % vec) == 0 && (d % vec) == 0;
     const int NB = (F + 15) / 16;
-    if (aligned && NB >= 1 && NB <= 6) {  // NB 7-8 exceed 256 VGPRs: scalar path
-        switch (NB) {
-            case 1: launch_fwd_nb<1>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-            case 2: launch_fwd_nb<2>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-            case 3: launch_fwd_nb<3>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-            case 4: launch_fwd_nb<4>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-            case 5: launch_fwd_nb<5>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-            case 6: launch_fwd_nb<6>(s, cus, dtype, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding); break;
-        }
-    } else {
+    GatherArgs ga{};
+    bool done = false;
+    if (fwd_aligned(dtype, d, x, x_ld, ys, ys_ld))
+        done = dtype == DLRM_F32
+                   ? dispatch_fwd<float, false>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga)
+                   : dispatch_fwd<uint16_t, false>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga);
+    if (!done) {  // NB > 6 would exceed 256 VGPRs; odd alignments
         const int W = d + F * (F - 1) / 2 + padding;
         const unsigned g = grid_for((int64_t)B * W, 256, cus);
         if (dtype == DLRM_F32)
@@ -376,6 +455,27 @@ int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
                                x_ld, (uint16_t*)ys, ys_ld, (uint16_t*)out, out_ld, padding);
     }
     return ctx_hip(ctx, hipGetLastError(), "interact_fwd launch");
+}
+
+// maplookup(PreallocationStrategy(d)) + DotInteraction in one launch.  Returns
+// DLRM_E_UNSUPPORTED when the shape/alignment has no fused kernel (the caller then runs
+// the two operators separately).
+int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
+                               const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                               const void* x, int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld,
+                               int padding) {
+    if (B == 0) return DLRM_OK;
+    const int F = T_ + 1;
+    const int NB = (F + 15) / 16;
+    if (!tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, ys, ys_ld) || NB > 6) return DLRM_E_UNSUPPORTED;
+    hipStream_t s = ctx_stream(ctx);
+    const int cus = ctx_num_cus(ctx);
+    GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
+    const bool ok = dtype == DLRM_F32
+                        ? dispatch_fwd<float, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga)
+                        : dispatch_fwd<uint16_t, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga);
+    if (!ok) return DLRM_E_UNSUPPORTED;
+    return ctx_hip(ctx, hipGetLastError(), "lookup_interact_fwd launch");
 }
 
 template <typename T>
@@ -398,7 +498,11 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     const int NB = (F + 15) / 16;
-    if (NB >= 1 && NB <= 7) {  // NB = 8 would need > 64 KB of dynamic LDS
+    const int esz = dtype == DLRM_F32 ? 4 : 2;
+    const bool aligned = d % 4 == 0 && (uintptr_t)dout % (4 * esz) == 0 && (uintptr_t)t % (4 * esz) == 0 &&
+                         (dout_ld % 4) == 0 && (t_ld % 4) == 0 && (uintptr_t)dx % 16 == 0 &&
+                         (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 && (dt_ld % 4) == 0;
+    if (aligned && NB >= 1 && NB <= 7) {  // NB = 8 would need > 64 KB of dynamic LDS
         if (dtype == DLRM_F32) dispatch_bwd<float>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
         else dispatch_bwd<uint16_t>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
     } else {

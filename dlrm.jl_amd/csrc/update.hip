@@ -205,10 +205,7 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
     __syncthreads();
 
     // ---- chunk and hot-segment work lists
-    int32_t* ch_beg = ix.ch_beg + off;
-    int32_t* ch_end = ix.ch_end + off;
-    uint32_t* ch_row = ix.ch_row + off;
-    int32_t* ch_slot = ix.ch_slot + off;
+    int4* chunks = ix.chunks + off;
     uint32_t* hot_row = ix.hot_row + off;
     int32_t* hot_slot0 = ix.hot_slot0 + off;
     int32_t* hot_n = ix.hot_n + off;
@@ -228,10 +225,7 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
             for (int k = 0; k < nch; ++k) {
                 const int cid = C + c0 + k;
                 const int b0 = beg + k * kChunk;
-                ch_beg[cid] = b0;
-                ch_end[cid] = b0 + kChunk < end ? b0 + kChunk : end;
-                ch_row[cid] = row;
-                ch_slot[cid] = hot ? HC + hc0 + k : -1;
+                chunks[cid] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, (int)row, hot ? HC + hc0 + k : -1);
             }
             if (hot) {
                 hot_row[H + h0] = row;
@@ -280,69 +274,106 @@ struct ApplyGeom {
 };
 
 // grad rows are fp32 or bf16; D elements = VPR vectors of 16 B of the GRAD dtype.
+// One lane group per chunk, no loop over chunks: the grid covers the worst case (one chunk per
+// lookup) and groups past the table's chunk count exit at once.  The dependency chain is
+// descriptor -> {positions -> grad rows, table row} -> write, with up to 8 grad rows in flight.
+template <typename TT, int NE>
+__device__ __forceinline__ void load_row(const TT* row, int c0, float* f) {
+    constexpr int BYTES = (int)sizeof(TT) * NE;
+    if constexpr (BYTES % 16 == 0) {
+        typedef Vec<TT> V;
+#pragma unroll
+        for (int k = 0; k < BYTES / 16; ++k) V::to_f32(*((const typename V::type*)(row + c0) + k), f + k * V::N);
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) f[e] = to_f32(row[c0 + e]);
+    }
+}
+
+template <typename TT, int NE>
+__device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
+    constexpr int BYTES = (int)sizeof(TT) * NE;
+    if constexpr (BYTES % 16 == 0) {
+        typedef Vec<TT> V;
+#pragma unroll
+        for (int k = 0; k < BYTES / 16; ++k) *((typename V::type*)(row + c0) + k) = V::from_f32(f + k * V::N);
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) row[c0 + e] = from_f32<TT>(f[e]);
+    }
+}
+
 template <typename TT, typename GT, int VPR>
 __global__ __launch_bounds__(256) void sgd_chunks_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int L,
                                                          const GT* __restrict__ grad, int64_t grad_ld,
-                                                         int64_t grad_offset, float lr, float* __restrict__ partial,
-                                                         int chunks_per_block) {
+                                                         int64_t grad_offset, float lr, float* __restrict__ partial) {
     typedef ApplyGeom<TT, GT, VPR> G;
     typedef typename G::GV GV;
     constexpr int NE = GV::N;
     constexpr int D = VPR * NE;
+    constexpr int U = 8;
     const int t = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane / G::LPR, v = lane % G::LPR;
     if (g >= G::RPW) return;
+    const int cid = (blockIdx.x * (blockDim.x >> 6) + w) * G::RPW + g;
     const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
+    if (cid >= nchunks) return;
     const int64_t off = (int64_t)t * ix.cap;
+    const int4 cd = ix.chunks[off + cid];
+    const int beg = cd.x, end = cd.y, slot = cd.w;
+    TT* row = (TT*)tabs[t].data + (int64_t)(uint32_t)cd.z * D;
+    // table row early: its latency overlaps the position -> gradient chain
+    float tv[G::VPL][NE];
+    if (slot < 0) {
+#pragma unroll
+        for (int j = 0; j < G::VPL; ++j) load_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
+    }
     const int32_t* perm = ix.perm + off;
     const GT* gbase = grad + grad_offset + (int64_t)t * D;
-    TT* table = (TT*)tabs[t].data;
-    const int waves_per_block = blockDim.x >> 6;
-    for (int cid = blockIdx.x * chunks_per_block + w * G::RPW + g; cid < (blockIdx.x + 1) * chunks_per_block && cid < nchunks;
-         cid += waves_per_block * G::RPW) {
-        const int beg = ix.ch_beg[off + cid], end = ix.ch_end[off + cid];
-        float acc[G::VPL][NE];
+    float acc[G::VPL][NE];
+#pragma unroll
+    for (int j = 0; j < G::VPL; ++j)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
+    for (int i = beg; i < end; i += U) {
+        int32_t p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = (i + u < end) ? perm[i + u] : -1;
+        typename GV::type gv[U][G::VPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p[u] >= 0) {
+                const GT* gr = gbase + (int64_t)(p[u] / L) * grad_ld;
+#pragma unroll
+                for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p[u] >= 0) {
+#pragma unroll
+                for (int j = 0; j < G::VPL; ++j) {
+                    float f[NE];
+                    GV::to_f32(gv[u][j], f);
+#pragma unroll
+                    for (int e = 0; e < NE; ++e) acc[j][e] += f[e];  // ascending position order
+                }
+            }
+    }
+    if (slot < 0) {
+#pragma unroll
+        for (int j = 0; j < G::VPL; ++j) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) tv[j][e] = __builtin_fmaf(-lr, acc[j][e], tv[j][e]);
+            store_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
+        }
+    } else {
+        float* pr = partial + ((int64_t)t * ix.hot_cap + slot) * D;
 #pragma unroll
         for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
-            for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-        for (int i = beg; i < end; i += 4) {
-            typename GV::type gv[4][G::VPL];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (i + u < end) {
-                    const int64_t b = perm[i + u] / L;
-                    const GT* gr = gbase + b * grad_ld;
-#pragma unroll
-                    for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (i + u < end) {
-#pragma unroll
-                    for (int j = 0; j < G::VPL; ++j) {
-                        float f[NE];
-                        GV::to_f32(gv[u][j], f);
-#pragma unroll
-                        for (int e = 0; e < NE; ++e) acc[j][e] += f[e];
-                    }
-                }
-            }
-        }
-        const int slot = ix.ch_slot[off + cid];
-        if (slot < 0) {
-            TT* row = table + (int64_t)ix.ch_row[off + cid] * D;
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j) rmw_row<TT, NE>(row, (v + j * 64) * NE, acc[j], lr);
-        } else {
-            float* pr = partial + ((int64_t)t * ix.hot_cap + slot) * D;
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j)
-#pragma unroll
-                for (int e = 0; e < NE; ++e) pr[(v + j * 64) * NE + e] = acc[j][e];
-        }
+            for (int e = 0; e < NE; e += 4)
+                *(f32x4*)(pr + (v + j * 64) * NE + e) = f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
     }
 }
 
@@ -389,15 +420,16 @@ __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDes
     TT* table = (TT*)tabs[t].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int cid = (int)(e / D), c = (int)(e % D);
-        const int beg = ix.ch_beg[off + cid], end = ix.ch_end[off + cid];
+        const int4 cd = ix.chunks[off + cid];
+        const int beg = cd.x, end = cd.y;
         float acc = 0.0f;
         for (int i = beg; i < end; ++i) {
             const int64_t b = ix.perm[off + i] / L;
             acc += to_f32(grad[b * grad_ld + grad_offset + (int64_t)t * D + c]);
         }
-        const int slot = ix.ch_slot[off + cid];
+        const int slot = cd.w;
         if (slot < 0) {
-            TT* row = table + (int64_t)ix.ch_row[off + cid] * D;
+            TT* row = table + (int64_t)(uint32_t)cd.z * D;
             row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
         } else {
             partial[((int64_t)t * ix.hot_cap + slot) * D + c] = acc;
@@ -469,10 +501,10 @@ template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
                              int64_t grad_ld, int64_t grad_offset, float lr, float* partial, int64_t N) {
     typedef ApplyGeom<TT, GT, VPR> G;
-    const int per_block = 4 * G::RPW * 4;  // 4 waves x RPW groups x 4 rounds
+    const int per_block = 4 * G::RPW;  // 4 waves x RPW lane groups, one chunk each
     const int64_t gx = (N + per_block - 1) / per_block;
     hipLaunchKernelGGL((sgd_chunks_kernel<TT, GT, VPR>), dim3((unsigned)(gx < 1 ? 1 : gx), T_), dim3(256), 0, s, ix,
-                       tabs, L, (const GT*)grad, grad_ld, grad_offset, lr, partial, per_block);
+                       tabs, L, (const GT*)grad, grad_ld, grad_offset, lr, partial);
     const int64_t hx = (ix.hot_cap + 4 * G::RPW - 1) / (4 * G::RPW);
     hipLaunchKernelGGL((sgd_hot_kernel<TT, GT, VPR>), dim3((unsigned)(hx < 1 ? 1 : (hx > 64 ? 64 : hx)), T_), dim3(256),
                        0, s, ix, tabs, lr, partial);

@@ -17,7 +17,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .runtime import context, dtype_code, itype_code, ptr
+from .runtime import context, dtype_code, itype_code, ptr, require_device
 
 
 class SimpleEmbedding:
@@ -124,6 +124,8 @@ class PackedIndices:
     def __init__(self, sparse, device=None, dtype=None):
         if isinstance(sparse, PackedIndices):
             self.__dict__.update(sparse.__dict__)
+            if device is not None and self.data.device != torch.device(device):
+                self.data = self.data.to(device)
             return
         if isinstance(sparse, torch.Tensor):
             if sparse.dim() == 2:
@@ -155,6 +157,10 @@ class PackedIndices:
         self.data = data.contiguous()
         self.T, self.B, self.L = int(T), int(B), int(L)
 
+    def on(self, device):
+        """This index set on `device` (self if already there)."""
+        return self if self.data.device == torch.device(device) else PackedIndices(self, device=device)
+
     @property
     def stride(self):
         return self.data.stride(0) if self.T > 0 else 0
@@ -173,6 +179,7 @@ def maplookup(strategy, tables, sparse, *, index_base=1, out=None, check_bounds=
     Raises BoundsError on an out-of-range index when check_bounds (synchronises)."""
     ts = as_table_set(tables)
     idx = PackedIndices(sparse, device=ts.device)
+    require_device(idx.data, ts.device, "indices")
     if idx.T != len(ts):
         raise ValueError(f"{idx.T} index arrays for {len(ts)} tables")
     P = strategy.prealloc if isinstance(strategy, PreallocationStrategy) else 0
@@ -181,6 +188,7 @@ def maplookup(strategy, tables, sparse, *, index_base=1, out=None, check_bounds=
         out = torch.empty((idx.B, width), dtype=ts.dtype, device=ts.device)
     elif out.shape[0] != idx.B or out.shape[1] < width or out.stride(1) != 1 or out.dtype != ts.dtype:
         raise ValueError("maplookup: `out` has the wrong shape/dtype/layout")
+    require_device(out, ts.device, "out")
     ctx = ts.ctx
     ctx.check(ctx.lib.dlrm_maplookup(ctx.bind(), ts.handle, ptr(idx.data), idx.itype, idx.stride, index_base,
                                      idx.B, idx.L, ptr(out), out.stride(0), P))

@@ -9,9 +9,10 @@ does for the sparse half of the model on one batch:
     dx, dt = dot_back(dot, dout, T, d, padding)                    interact.jl:442-445
     update!(Descent(lr), tables, maplookup_pullback(dt), indexers) train.jl:283-290
 
-All buffers are allocated once; a step issues 4 kernel launches on the current stream
-(lookup, interaction fwd, interaction bwd, indexer sort) + 2 for the update, with no
-host synchronisation, so the whole step can be captured in a torch.cuda graph.  With
+All buffers are allocated once; a step issues 5 kernel launches on the current stream
+(fused lookup + interaction fwd, indexer sort, interaction bwd, 2 for the update) with no
+host synchronisation, so the whole step can be captured in a torch.cuda graph
+(`fused=False` runs maplookup and the interaction as two launches, like the reference).  With
 `overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a
 side stream concurrently with the lookup and the interaction.
 """
@@ -20,13 +21,13 @@ import torch
 from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices
 from .interact import interaction_sizes
-from .runtime import dtype_code, ptr
+from .runtime import dtype_code, ptr, require_device
 from .update import SparseIndexer
 
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=False, pad_to=1):
+                 overlap_indexer=False, pad_to=1, fused=True):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -35,6 +36,7 @@ class HotPath:
         self.lr = float(lr)
         self.index_base = int(index_base)
         self.deterministic = deterministic
+        self.fused = fused
         _, self.width, self.padding = interaction_sizes(self.d, self.F, pad_to)
         dev, dt = self.ts.device, self.ts.dtype
         self.ys = torch.empty((self.B, self.F * self.D), dtype=dt, device=dev)
@@ -65,6 +67,13 @@ class HotPath:
                                                ptr(self.ys), self.ys.stride(0), ptr(self.out), self.out.stride(0),
                                                self.padding))
 
+    def lookup_interact_fwd(self, x, idx):
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_lookup_interact_fwd(h, self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
+                                                      self.index_base, self.B, self.L, ptr(x), x.stride(0),
+                                                      ptr(self.ys), self.ys.stride(0), ptr(self.out),
+                                                      self.out.stride(0), self.padding))
+
     def build_indexer(self, idx):
         h = self.ctx.bind()
         self._check(self.lib.dlrm_indexer_build(h, self.indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
@@ -86,6 +95,20 @@ class HotPath:
                                              ptr(self.dt), _lib.F32, self.dt.stride(0), self.d, self.lr))
 
     # -- step --------------------------------------------------------------------------
+    def validate(self, x, idx, dout=None):
+        """Host-side shape/device checks (call once per new buffer set; the step itself does not)."""
+        dev = self.ts.device
+        require_device(x, dev, "x")
+        require_device(idx.data, dev, "indices")
+        if x.shape != (self.B, self.d) or x.dtype != self.ts.dtype or x.stride(1) != 1:
+            raise ValueError(f"x must be [{self.B}][{self.d}] {self.ts.dtype}")
+        if (idx.T, idx.B, idx.L) != (self.T, self.B, self.L):
+            raise ValueError("indices do not match the engine's (tables, batch, lookups)")
+        if dout is not None:
+            require_device(dout, dev, "dout")
+            if dout.shape != (self.B, self.width) or dout.dtype != self.ts.dtype or dout.stride(1) != 1:
+                raise ValueError(f"dout must be [{self.B}][{self.width}] {self.ts.dtype}")
+
     def forward(self, x, idx):
         if self.overlap_indexer:
             main = torch.cuda.current_stream(self.ts.device)
@@ -94,8 +117,11 @@ class HotPath:
                 self.build_indexer(idx)
                 self._indexer_done = torch.cuda.Event()
                 self._indexer_done.record(self._side)
-        self.lookup(idx)
-        self.interact_fwd(x)
+        if self.fused:
+            self.lookup_interact_fwd(x, idx)
+        else:
+            self.lookup(idx)
+            self.interact_fwd(x)
         return self.out
 
     def backward(self, idx, dout):

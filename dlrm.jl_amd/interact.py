@@ -12,7 +12,7 @@ Shapes (torch, row-major = the transpose of the Julia matrices):
 """
 import torch
 
-from .runtime import context, dtype_code, ptr
+from .runtime import context, dtype_code, ptr, require_device
 
 POST_INTERACTION_PAD_TO_MUL = 1  # model.jl:32
 
@@ -54,6 +54,10 @@ class DotInteraction:
         _, padded, padding = interaction_sizes(d, F, self.pad_to)
         if out is None:
             out = torch.empty((B, padded), dtype=x.dtype, device=x.device)
+        for name, t in (("x", x), ("ys", ys), ("out", out)):
+            require_device(t, x.device, name)
+        if out.shape[0] != B or out.shape[1] < padded or out.stride(1) != 1:
+            raise ValueError("DotInteraction: `out` has the wrong shape/layout")
         ctx = context(x.device)
         ctx.check(ctx.lib.dlrm_interact_fwd(ctx.bind(), dtype_code(x.dtype), d, F, B, ptr(x), x.stride(0), ptr(ys),
                                             ys.stride(0), ptr(out), out.stride(0), padding))
@@ -74,6 +78,11 @@ def dot_back(dot, delta, t, xlen, padding, *, dx=None, dt=None):
         dt = torch.empty((B, F * d), dtype=torch.float32, device=delta.device)
     if delta.dtype != t.dtype:
         raise TypeError("dot_back: Δ and T must share a dtype")
+    for name, a in (("Δ", delta), ("T", t), ("dx", dx), ("dt", dt)):
+        require_device(a, delta.device, name)
+    if (t.shape[0] != B or delta.stride(1) != 1 or t.stride(1) != 1 or dx.shape != (B, d) or
+            dt.shape[0] != B or dt.shape[1] < F * d or dx.dtype != torch.float32 or dt.dtype != torch.float32):
+        raise ValueError("dot_back: inconsistent shapes/dtypes")
     ctx = context(delta.device)
     ctx.check(ctx.lib.dlrm_interact_bwd(ctx.bind(), dtype_code(delta.dtype), d, F, B, ptr(delta), delta.stride(0),
                                         padding, ptr(t), t.stride(0), ptr(dx), dx.stride(0), ptr(dt), dt.stride(0)))

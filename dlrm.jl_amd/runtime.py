@@ -62,6 +62,17 @@ def context(device=None):
         return ctx
 
 
+def require_device(t, device, name):
+    """Every buffer handed to a kernel must be a CUDA tensor on the ctx's device: a host
+    pointer would fault the GPU.  Raises ValueError before anything is launched."""
+    if t is None:
+        return
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch tensor, got {type(t).__name__}")
+    if not t.is_cuda or (device is not None and t.device != torch.device(device)):
+        raise ValueError(f"{name} lives on {t.device}, the kernel runs on {device}")
+
+
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices, as_table_set
-from .runtime import context, dtype_code, ptr
+from .runtime import context, dtype_code, ptr, require_device
 
 
 class Descent:
@@ -62,7 +62,7 @@ def maplookup_pullback(strategy_prealloc, tables, sparse, dy):
     """Pullback of maplookup(PreallocationStrategy(P), tables, sparse) given dy [B][P + D*T]
     (e.g. dt_reshaped from dot_back): views, no arithmetic (the rows 1:P belong to x)."""
     ts = as_table_set(tables)
-    idx = sparse if isinstance(sparse, PackedIndices) else PackedIndices(sparse, device=ts.device)
+    idx = PackedIndices(sparse, device=ts.device)
     return [SparseEmbeddingUpdate(dy, strategy_prealloc + t * ts.D, ts.D, idx, t) for t in range(len(ts))]
 
 
@@ -84,7 +84,10 @@ class SparseIndexer:
         """Dedupes `indices` (asynchronous).  May run on a side stream during the forward pass;
         pass prebuilt=True to update_ afterwards."""
         ts = as_table_set(tables)
-        idx = indices if isinstance(indices, PackedIndices) else PackedIndices(indices, device=ts.device)
+        idx = PackedIndices(indices, device=ts.device)
+        require_device(idx.data, ts.device, "indices")
+        if idx.B * idx.L > self.capacity or idx.T != self.num_tables:
+            raise ValueError("SparseIndexer: indices exceed the capacity / table count it was created for")
         self.ctx.check(self.ctx.lib.dlrm_indexer_build(self.ctx.bind(), self.handle, ts.handle, ptr(idx.data),
                                                        idx.itype, idx.stride, index_base, idx.B, idx.L))
         self._built_from = idx
@@ -143,13 +146,18 @@ def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, ind
     grad = g0.grad
     if grad.stride(1) != 1:
         raise ValueError("gradient rows must be contiguous")
-    idx = g0.indices
+    require_device(grad, ts.device, "gradient")
+    idx = g0.indices.on(ts.device)
+    if grad.shape[0] != idx.B:
+        raise ValueError(f"gradient has {grad.shape[0]} rows for a batch of {idx.B}")
     flags = 0
     ix = None
     if deterministic:
         if indexers is None:
             indexers = SparseIndexer(len(ts), idx.B * idx.L, ts.device)
         ix = indexers
+        if ix.num_tables != len(ts) or ix.capacity < idx.B * idx.L:
+            raise ValueError("SparseIndexer too small for this batch / table set")
         if prebuilt:
             flags |= _lib.UPDATE_PREBUILT
     else:

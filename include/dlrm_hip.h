@@ -116,6 +116,18 @@ int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
                       const void* x, int64_t x_ld, void* ys, int64_t ys_ld,
                       void* out, int64_t out_ld, int padding);
 
+/* maplookup(PreallocationStrategy(d), tables, sparse) followed by (dot::DotInteraction)(x, ys)
+ * as ONE launch (model.jl:161-163 with the bottom MLP already applied): every gathered row is
+ * loaded once into MFMA fragments and written to ys from registers, so ys is never re-read.
+ * ys and out receive exactly what dlrm_maplookup(out_offset = d) + dlrm_interact_fwd write
+ * (bit-identical); shapes without a fused kernel fall back to those two launches.
+ * Requires tables->dim == d; dtype is the tables' dtype. */
+int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tables,
+                             const void* indices, int itype, int64_t table_stride, int index_base,
+                             int batch, int lookups,
+                             const void* x, int64_t x_ld, void* ys, int64_t ys_ld,
+                             void* out, int64_t out_ld, int padding);
+
 /* dot_back(dot, dout, t, d, padding): S_b = symmetric zero-diagonal unpack of
  * dout[b][d : d + F(F-1)/2];  dt[b] = S_b T_b  ([F][d], fp32, x-rows included as the
  * reference returns them);  dx[b] = dout[b][0:d] + dt[b][0:d]  (fp32).

@@ -367,3 +367,46 @@ def test_full_size_properties_metric_config(pkg, gpu):
         ref = torch.zeros((rows[t], D), device=gpu, dtype=torch.float64)
         ref.index_add_(0, idx[t].long(), gi[:, t * D:(t + 1) * D].double())
         assert torch.equal(zt[t].data, (-ref).float())
+
+
+# ------------------------------------------------------------------ fused lookup + interaction
+@pytest.mark.parametrize("rows,D,B,L,dtype", [
+    ([1000] * 7, 16, 128, 1, torch.float32), ([1000] * 7, 16, 128, 10, torch.float32),
+    ([5, 100000, 3, 77] * 6 + [9, 10], 128, 300, 1, torch.float32), ([50] * 40, 32, 33, 3, torch.float32),
+    ([5, 100000, 3, 77] * 6 + [9, 10], 128, 200, 1, torch.bfloat16), ([60] * 12, 64, 70, 4, torch.bfloat16),
+    ([7] * 3, 4, 9, 2, torch.float32)])
+def test_fused_lookup_interaction_equals_two_operators(pkg, gpu, rows, D, B, L, dtype):
+    rng = np.random.default_rng(len(rows) * D + L)
+    tabs = dev_tables(rand_tables(rng, rows, D), gpu, dtype)
+    idx = torch.from_numpy(rand_indices(rng, rows, B, L)).reshape(len(rows), B, L).to(torch.int32).to(gpu)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), B, L, index_base=0, fused=True)
+    p = pkg.PackedIndices(idx)
+    hp.validate(x, p)
+    hp.forward(x, p)
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), tabs, p, index_base=0)
+    out = pkg.DotInteraction()(x, ys)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    assert torch.equal(hp.ys, ys)    # lookup output + fast_vcat: bit-identical
+    assert torch.equal(hp.out, out)  # same MFMA order: bit-identical
+
+
+def test_fused_bounds_error(pkg, gpu):
+    tabs = [torch.ones((4, 16), device=gpu), torch.ones((4, 16), device=gpu)]
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), 2, 1, index_base=0)
+    x = torch.zeros((2, 16), device=gpu)
+    hp.forward(x, pkg.PackedIndices(torch.tensor([[0, 1], [2, 4]], dtype=torch.int32, device=gpu)))
+    with pytest.raises(pkg.BoundsError):
+        hp.check_bounds()
+    assert torch.equal(hp.ys[0, 16:], torch.ones(32, device=gpu))  # valid rows still gathered
+
+
+def test_host_tensors_are_rejected_before_launch(pkg, gpu):
+    x = torch.zeros((4, 16))
+    ys = torch.zeros((4, 32), device=gpu)
+    with pytest.raises(ValueError):
+        pkg.DotInteraction()(x.to(gpu), ys, out=torch.zeros((4, 17)))
+    hp = pkg.HotPath(pkg.EmbeddingTableSet([torch.zeros((5, 16), device=gpu)]), 4, 1, index_base=0)
+    with pytest.raises(ValueError):
+        hp.validate(x, pkg.PackedIndices(torch.zeros((1, 4), dtype=torch.int32)))
