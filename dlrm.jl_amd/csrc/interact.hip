@@ -323,8 +323,9 @@ __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, 
                         if (f < F) {
                             const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
                             *(f32x4_t*)(dt + b * dt_ld + (int64_t)f * d + n0) = v;
-                            if (f == 0) {
-                                const f32x4_t xo = load4_f32(ob + n0);
+                            if (f == 0) {  // dout rows need no alignment: scalar reads
+                                const f32x4_t xo = f32x4_t{to_f32(ob[n0]), to_f32(ob[n0 + 1]), to_f32(ob[n0 + 2]),
+                                                           to_f32(ob[n0 + 3])};
                                 *(f32x4_t*)(dx + b * dx_ld + n0) = xo + v;
                             }
                         }
@@ -499,8 +500,7 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
     const int cus = ctx_num_cus(ctx);
     const int NB = (F + 15) / 16;
     const int esz = dtype == DLRM_F32 ? 4 : 2;
-    const bool aligned = d % 4 == 0 && (uintptr_t)dout % (4 * esz) == 0 && (uintptr_t)t % (4 * esz) == 0 &&
-                         (dout_ld % 4) == 0 && (t_ld % 4) == 0 && (uintptr_t)dx % 16 == 0 &&
+    const bool aligned = d % 4 == 0 && (uintptr_t)t % (4 * esz) == 0 && (t_ld % 4) == 0 && (uintptr_t)dx % 16 == 0 &&
                          (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 && (dt_ld % 4) == 0;
     if (aligned && NB >= 1 && NB <= 7) {  // NB = 8 would need > 64 KB of dynamic LDS
         if (dtype == DLRM_F32) dispatch_bwd<float>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
