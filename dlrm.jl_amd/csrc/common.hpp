@@ -78,8 +78,10 @@ struct IndexerDev {
     int32_t* perm;         // sorted positions (valid prefix)
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
-    int4* chunks;          // {beg, end, row, slot}: slot < 0 = single-chunk segment
+    int4* chunks;          // {beg, end, row, -1} single-chunk segment | {beg, end, hot id, slot} hot chunk
     uint32_t* hot_row; int32_t* hot_slot0; int32_t* hot_n;
+    int32_t* hot_cnt;      // per hot segment arrival counter (zeroed by the build, reset by the last arriver)
+    uint64_t* key64;       // rank-sort scratch: (row << 32) | position
     int32_t* counts;       // [T][8]: U, chunks, hot, hot_chunks, nvalid
     int64_t cap;
     int64_t hot_cap;       // hot-chunk slots per table

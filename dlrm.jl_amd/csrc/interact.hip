@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void interact_fwd_kernel(int d, int F, int B, 
                                                            int64_t out_ld, int padding, GatherArgs ga) {
     typedef Frag<T> FR;
     typedef typename FR::type frag;
-    constexpr int UU = 4;  // column steps whose loads are issued together
+    constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
     __shared__ float stage_all[4][kStage];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;

@@ -15,9 +15,10 @@
 //     positions (hot rows of small tables: a 3-row table gets ~680 hits per row at B=2048)
 //     are split so that no wave serialises on a hot row.
 //  2. sgd_chunks (grid over all chunks): one lane group per chunk streams its grad rows in
-//     ascending position order (fp32 sum, 16-B lanes, 4 rows in flight), then either
-//     read-modify-writes the table row once (single-chunk segment) or stores a partial sum.
-//  3. sgd_hot: hot segments add their partials in chunk order and write the row once.
+//     ascending position order (fp32 sum, 16-B lanes, 8 rows in flight), then either
+//     read-modify-writes the table row once (single-chunk segment) or publishes a partial
+//     sum; the last chunk of a hot segment to arrive (agent-scope ticket) adds the
+//     partials in chunk order and writes the row once.
 // Every touched row is written exactly once, with a summation order fixed by positions:
 // bitwise reproducible.  DLRM_UPDATE_ATOMIC instead adds -lr*g straight into the table
 // with global_atomic_add_f32 (no sort, non-deterministic rounding order).
@@ -66,6 +67,81 @@ struct SortLds {
     int wtot[2 * kBuildWaves];
     int nvalid;
 };
+
+// Segments + chunk/hot work lists from a table's sorted (row, position) arrays; one
+// 1024-thread workgroup per table.  K/V may live in LDS or global memory.
+__device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, const int32_t* V, int N,
+                               uint32_t sentinel, SortLds& sl) {
+    const int tid = threadIdx.x;
+    const int64_t off = (int64_t)t * ix.cap;
+
+    // ---- segments: one per distinct valid row; perm = sorted positions
+    if (tid == 0) sl.nvalid = 0;
+    __syncthreads();
+    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+    int32_t* perm = ix.perm + off;
+    int U = 0;
+    for (int tile = 0; tile < N; tile += kBuildThreads) {
+        const int i = tile + tid;
+        const uint32_t k = i < N ? K[i] : sentinel;
+        const bool live = i < N && k != sentinel;
+        const bool head = live && (i == 0 || K[i - 1] != k);
+        if (live) {
+            perm[i] = V[i];
+            if (i + 1 == N || K[i + 1] == sentinel) sl.nvalid = i + 1;
+        }
+        int tot;
+        const int ex = block_scan_excl(head ? 1 : 0, sl.wtot, &tot);
+        if (head) {
+            seg_start[U + ex] = i;
+            seg_row[U + ex] = k;
+        }
+        U += tot;
+    }
+    __syncthreads();
+    const int nvalid = sl.nvalid;
+    if (tid == 0) seg_start[U] = nvalid;
+    __syncthreads();
+
+    // ---- chunk and hot-segment work lists
+    int4* chunks = ix.chunks + off;
+    uint32_t* hot_row = ix.hot_row + off;
+    int32_t* hot_slot0 = ix.hot_slot0 + off;
+    int32_t* hot_n = ix.hot_n + off;
+    int C = 0, H = 0, HC = 0;
+    for (int tile = 0; tile < U; tile += kBuildThreads) {
+        const int s = tile + tid;
+        int beg = 0, end = 0;
+        if (s < U) { beg = seg_start[s]; end = seg_start[s + 1]; }
+        const int nch = (end - beg + kChunk - 1) / kChunk;
+        const bool hot = nch > 1;
+        int ctot, htot, hctot;
+        const int c0 = block_scan_excl(nch, sl.wtot, &ctot);
+        const int h0 = block_scan_excl(hot ? 1 : 0, sl.wtot, &htot);
+        const int hc0 = block_scan_excl(hot ? nch : 0, sl.wtot, &hctot);
+        if (s < U) {
+            const uint32_t row = seg_row[s];
+            for (int k = 0; k < nch; ++k) {
+                const int cid = C + c0 + k;
+                const int b0 = beg + k * kChunk;
+                chunks[cid] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, hot ? H + h0 : (int)row,
+                                        hot ? HC + hc0 + k : -1);
+            }
+            if (hot) {
+                hot_row[H + h0] = row;
+                hot_slot0[H + h0] = HC + hc0;
+                hot_n[H + h0] = nch;
+                ix.hot_cnt[off + H + h0] = 0;  // arrival counter, reset every build
+            }
+        }
+        C += ctot; H += htot; HC += hctot;
+    }
+    if (tid == 0) {
+        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
+    }
+}
 
 template <bool IN_LDS>
 __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
@@ -172,73 +248,72 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
             __syncthreads();
         }
     }
-    const uint32_t* K = kbuf[passes & 1];
-    const int32_t* V = vbuf[passes & 1];
+    build_segments(ix, t, kbuf[passes & 1], vbuf[passes & 1], N, sentinel, sl);
+}
 
-    // ---- segments: one per distinct valid row; perm = sorted positions
-    if (tid == 0) sl.nvalid = 0;
-    __syncthreads();
-    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
-    uint32_t* seg_row = ix.seg_row + off;
-    int32_t* perm = ix.perm + off;
-    int U = 0;
-    for (int tile = 0; tile < N; tile += kBuildThreads) {
-        const int i = tile + tid;
-        const uint32_t k = i < N ? K[i] : sentinel;
-        const bool live = i < N && k != sentinel;
-        const bool head = live && (i == 0 || K[i - 1] != k);
-        if (live) {
-            perm[i] = V[i];
-            if (i + 1 == N || K[i + 1] == sentinel) sl.nvalid = i + 1;
-        }
-        int tot;
-        const int ex = block_scan_excl(head ? 1 : 0, sl.wtot, &tot);
-        if (head) {
-            seg_start[U + ex] = i;
-            seg_row[U + ex] = k;
-        }
-        U += tot;
-    }
-    __syncthreads();
-    const int nvalid = sl.nvalid;
-    if (tid == 0) seg_start[U] = nvalid;
-    __syncthreads();
 
-    // ---- chunk and hot-segment work lists
-    int4* chunks = ix.chunks + off;
-    uint32_t* hot_row = ix.hot_row + off;
-    int32_t* hot_slot0 = ix.hot_slot0 + off;
-    int32_t* hot_n = ix.hot_n + off;
-    int C = 0, H = 0, HC = 0;
-    for (int tile = 0; tile < U; tile += kBuildThreads) {
-        const int s = tile + tid;
-        int beg = 0, end = 0;
-        if (s < U) { beg = seg_start[s]; end = seg_start[s + 1]; }
-        const int nch = (end - beg + kChunk - 1) / kChunk;
-        const bool hot = nch > 1;
-        int ctot, htot, hctot;
-        const int c0 = block_scan_excl(nch, sl.wtot, &ctot);
-        const int h0 = block_scan_excl(hot ? 1 : 0, sl.wtot, &htot);
-        const int hc0 = block_scan_excl(hot ? nch : 0, sl.wtot, &hctot);
-        if (s < U) {
-            const uint32_t row = seg_row[s];
-            for (int k = 0; k < nch; ++k) {
-                const int cid = C + c0 + k;
-                const int b0 = beg + k * kChunk;
-                chunks[cid] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, (int)row, hot ? HC + hc0 + k : -1);
-            }
-            if (hot) {
-                hot_row[H + h0] = row;
-                hot_slot0[H + h0] = HC + hc0;
-                hot_n[H + h0] = nch;
-            }
-        }
-        C += ctot; H += htot; HC += hctot;
+// ---- rank sort (N <= kRankMax): three short kernels that use every CU instead of one
+// workgroup per table.  Keys are unique 64-bit (row << 32 | position), so a position's
+// place in the stable sort is simply the number of smaller keys; each lane streams the
+// table's keys through the scalar cache (uniform addresses -> s_load) and does one 64-bit
+// compare + add per key.
+constexpr int kRankMax = 2048;
+
+__global__ __launch_bounds__(256) void indexer_pack_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
+                                                           const void* __restrict__ idx, int itype, int64_t tstride,
+                                                           int base, int N, unsigned* __restrict__ err) {
+    const int t = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    const int64_t nrows = tabs[t].nrows;
+    const int64_t r = load_index(idx, itype, t * tstride + p) - base;
+    uint32_t key = (uint32_t)nrows;  // sentinel: sorts after every valid row
+    if (r >= 0 && r < nrows) key = (uint32_t)r;
+    else raise_index_error(err);
+    ix.key64[(int64_t)t * ix.cap + p] = ((uint64_t)key << 32) | (uint32_t)p;
+}
+
+__global__ __launch_bounds__(512) void indexer_rank_kernel(IndexerDev ix, int N) {
+    // the table's keys staged once in LDS; every lane then reads them back as 2-key
+    // broadcasts (ds_read_b128, same address in all lanes) with the compares pipelined
+    // behind in-order LDS returns.
+    __shared__ __attribute__((aligned(16))) uint64_t keys[kRankMax + 32];  // +32: ~0 padding for the prefetch
+    const int t = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t off = (int64_t)t * ix.cap;
+    const uint64_t* __restrict__ K = ix.key64 + off;
+    for (int i = threadIdx.x; i < kRankMax + 32; i += blockDim.x) keys[i] = i < N ? K[i] : ~0ull;
+    __syncthreads();
+    const uint64_t kp = p < N ? keys[p] : ~0ull;
+    const int n16 = (N + 15) & ~15;  // padding keys (~0) are never smaller than a real key
+    int c[4] = {0, 0, 0, 0};
+    const ulonglong2* k2 = (const ulonglong2*)keys;
+    // two 8-key batches in flight: batch b+1's LDS reads overlap batch b's compares
+    ulonglong2 va[4], vb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) va[k] = k2[k];
+    for (int q = 0; q < n16; q += 16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vb[k] = k2[(q + 8) / 2 + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] += (va[k].x < kp ? 1 : 0) + (va[k].y < kp ? 1 : 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) va[k] = k2[(q + 16) / 2 + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] += (vb[k].x < kp ? 1 : 0) + (vb[k].y < kp ? 1 : 0);
     }
-    if (tid == 0) {
-        int32_t* cnt = ix.counts + (int64_t)t * 8;
-        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
-    }
+    if (p >= N) return;
+    const int rank = c[0] + c[1] + c[2] + c[3];
+    ix.keys0[off + rank] = (uint32_t)(kp >> 32);
+    ix.vals0[off + rank] = p;
+}
+
+__global__ __launch_bounds__(kBuildThreads) void indexer_segments_kernel(IndexerDev ix,
+                                                                          const TableDesc* __restrict__ tabs, int N) {
+    __shared__ SortLds sl;
+    const int t = blockIdx.x;
+    const int64_t off = (int64_t)t * ix.cap;
+    build_segments(ix, t, ix.keys0 + off, ix.vals0 + off, N, (uint32_t)tabs[t].nrows, sl);
 }
 
 // Row read-modify-write of NE consecutive elements at element offset c0: row -= lr * acc,
@@ -322,7 +397,7 @@ __global__ __launch_bounds__(256) void sgd_chunks_kernel(IndexerDev ix, TableDes
     const int64_t off = (int64_t)t * ix.cap;
     const int4 cd = ix.chunks[off + cid];
     const int beg = cd.x, end = cd.y, slot = cd.w;
-    TT* row = (TT*)tabs[t].data + (int64_t)(uint32_t)cd.z * D;
+    TT* row = (TT*)tabs[t].data + (slot < 0 ? (int64_t)(uint32_t)cd.z * D : 0);
     // table row early: its latency overlaps the position -> gradient chain
     float tv[G::VPL][NE];
     if (slot < 0) {
@@ -375,37 +450,54 @@ __global__ __launch_bounds__(256) void sgd_chunks_kernel(IndexerDev ix, TableDes
             for (int e = 0; e < NE; e += 4)
                 *(f32x4*)(pr + (v + j * 64) * NE + e) = f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
     }
-}
-
-template <typename TT, typename GT, int VPR>
-__global__ __launch_bounds__(256) void sgd_hot_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, float lr,
-                                                      const float* __restrict__ partial) {
-    typedef ApplyGeom<TT, GT, VPR> G;
-    constexpr int NE = Vec<GT>::N;
-    constexpr int D = VPR * NE;
-    const int t = blockIdx.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int g = lane / G::LPR, v = lane % G::LPR;
-    if (g >= G::RPW) return;
-    const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
-    const int64_t off = (int64_t)t * ix.cap;
-    TT* table = (TT*)tabs[t].data;
-    const int per_block = (blockDim.x >> 6) * G::RPW;
-    for (int h = blockIdx.x * per_block + w * G::RPW + g; h < nhot; h += gridDim.x * per_block) {
-        const int s0 = ix.hot_slot0[off + h], n = ix.hot_n[off + h];
-        const float* pr = partial + ((int64_t)t * ix.hot_cap + s0) * D;
-        TT* row = table + (int64_t)ix.hot_row[off + h] * D;
+    // Hot rows: every chunk published its partial; the LAST chunk to arrive adds all partials
+    // of the segment in chunk order (deterministic whatever the arrival order) and writes the
+    // row once.  Hand-off = cdna_hip_programming.md Guideline 16: stores drained, agent-scope
+    // release, relaxed agent atomic ticket; the last arriver takes an agent-scope acquire
+    // before reading the other chunks' partials.  Placement-independent.
+    const bool hot = slot >= 0;
+    if (!__any(hot)) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait may be dropped (G16 P12)
+    const int h = cd.z;
+    int old = -1;
+    if (hot && v == 0) old = __hip_atomic_fetch_add(ix.hot_cnt + off + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, g * G::LPR, 64);
+    const int n = hot ? ix.hot_n[off + h] : 0;
+    const bool last = hot && old == n - 1;
+    if (!__any(last)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!last) return;
+    const int s0 = ix.hot_slot0[off + h];
+    TT* hrow = (TT*)tabs[t].data + (int64_t)ix.hot_row[off + h] * D;
+    const float* p0 = partial + ((int64_t)t * ix.hot_cap + s0) * D;
 #pragma unroll
-        for (int j = 0; j < G::VPL; ++j) {
-            float acc[NE];
+    for (int j = 0; j < G::VPL; ++j) {
+        const int c0 = (v + j * 64) * NE;
+        float hv[NE], sum[NE];
+        load_row<TT, NE>(hrow, c0, hv);
 #pragma unroll
-            for (int e = 0; e < NE; ++e) acc[e] = 0.0f;
-            for (int k = 0; k < n; ++k)
+        for (int e = 0; e < NE; ++e) sum[e] = 0.0f;
+        for (int k = 0; k < n; k += 4) {
+            f32x4 pv[4][NE / 4];
 #pragma unroll
-                for (int e = 0; e < NE; ++e) acc[e] += pr[(int64_t)k * D + (v + j * 64) * NE + e];
-            rmw_row<TT, NE>(row, (v + j * 64) * NE, acc, lr);
+            for (int u = 0; u < 4; ++u)
+                if (k + u < n)
+#pragma unroll
+                    for (int e = 0; e < NE; e += 4) pv[u][e / 4] = *(const f32x4*)(p0 + (int64_t)(k + u) * D + c0 + e);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k + u < n)
+#pragma unroll
+                    for (int e = 0; e < NE; ++e) sum[e] += pv[u][e / 4][e % 4];
         }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) hv[e] = __builtin_fmaf(-lr, sum[e], hv[e]);
+        store_row<TT, NE>(hrow, c0, hv);
     }
+    if (v == 0) __hip_atomic_store(ix.hot_cnt + off + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Generic (any D) versions: one thread per element column, loops over the chunk.
@@ -488,7 +580,16 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-    if (N <= kLdsSortMax)
+    if (N == 0) {
+        hipLaunchKernelGGL(indexer_segments_kernel, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, 0);
+    } else if (N <= kRankMax) {
+        const dim3 grid((unsigned)((N + 255) / 256), T_);
+        hipLaunchKernelGGL(indexer_pack_kernel, grid, dim3(256), 0, s, ix, tabs, idx, itype, tstride, base, (int)N,
+                           ctx_error_word(ctx));
+        // 512-thread blocks: two waves per SIMD hide each other's LDS latency
+        hipLaunchKernelGGL(indexer_rank_kernel, dim3((unsigned)((N + 511) / 512), T_), dim3(512), 0, s, ix, (int)N);
+        hipLaunchKernelGGL(indexer_segments_kernel, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, (int)N);
+    } else if (N <= kLdsSortMax)
         hipLaunchKernelGGL(indexer_build_kernel<true>, dim3(T_), dim3(kBuildThreads), indexer_lds_bytes(), s, ix, tabs,
                            idx, itype, tstride, base, B, L, ctx_error_word(ctx));
     else
@@ -505,9 +606,6 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     const int64_t gx = (N + per_block - 1) / per_block;
     hipLaunchKernelGGL((sgd_chunks_kernel<TT, GT, VPR>), dim3((unsigned)(gx < 1 ? 1 : gx), T_), dim3(256), 0, s, ix,
                        tabs, L, (const GT*)grad, grad_ld, grad_offset, lr, partial);
-    const int64_t hx = (ix.hot_cap + 4 * G::RPW - 1) / (4 * G::RPW);
-    hipLaunchKernelGGL((sgd_hot_kernel<TT, GT, VPR>), dim3((unsigned)(hx < 1 ? 1 : (hx > 64 ? 64 : hx)), T_), dim3(256),
-                       0, s, ix, tabs, lr, partial);
 }
 
 template <typename TT, typename GT>
