@@ -299,7 +299,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
         {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot_row, n * 4},
         {(void**)&ix->dev.hot_slot0, n * 4}, {(void**)&ix->dev.hot_n, n * 4},  {(void**)&ix->dev.counts, (size_t)T * 32},
-        {(void**)&ix->dev.hot_cnt, n * 4},   {(void**)&ix->dev.key64, n * 8},
+        {(void**)&ix->dev.hot_cnt, n * 4},
     };
     size_t total = 0;
     for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;

@@ -22,6 +22,13 @@ __device__ __forceinline__ void raise_index_error(unsigned* err) {
     __hip_atomic_fetch_or(err, kErrIndex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Orders one wave's LDS writes before its later LDS reads by other lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 // Round-to-nearest-even; NaN stays NaN (MI355X_MICROARCH.md, correctness boundaries).
@@ -81,7 +88,6 @@ struct IndexerDev {
     int4* chunks;          // {beg, end, row, -1} single-chunk segment | {beg, end, hot id, slot} hot chunk
     uint32_t* hot_row; int32_t* hot_slot0; int32_t* hot_n;
     int32_t* hot_cnt;      // per hot segment arrival counter (zeroed by the build, reset by the last arriver)
-    uint64_t* key64;       // rank-sort scratch: (row << 32) | position
     int32_t* counts;       // [T][8]: U, chunks, hot, hot_chunks, nvalid
     int64_t cap;
     int64_t hot_cap;       // hot-chunk slots per table

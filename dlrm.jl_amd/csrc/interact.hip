@@ -32,12 +32,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kStage = 1024;  // floats of output staging per wave
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // ---------------------------------------------------------------------------------- fwd
 // Fragment traits: fp32 -> v_mfma_f32_16x16x4_f32 with float4 loads (16 columns per step, 4
 // MFMA k-steps, one per component); bf16 -> v_mfma_f32_16x16x32_bf16 with 8-element loads

@@ -252,68 +252,165 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
 }
 
 
-// ---- rank sort (N <= kRankMax): three short kernels that use every CU instead of one
-// workgroup per table.  Keys are unique 64-bit (row << 32 | position), so a position's
-// place in the stable sort is simply the number of smaller keys; each lane streams the
-// table's keys through the scalar cache (uniform addresses -> s_load) and does one 64-bit
-// compare + add per key.
-constexpr int kRankMax = 2048;
+// ---- single-wave indexer (N <= kWaveSortMax): one 64-lane wave per table, no workgroup
+// barriers.  LSD radix over ceil(nbits/12) passes (two passes for the 24-bit Kaggle rows, one
+// for every table under 4096 rows).  Each pass: LDS histogram, wave-level exclusive scan of
+// the digit cursors, then the positions in order, 64 at a time: a lane finds the lanes with
+// its digit by ballots (multi-split), its rank among them, and the lowest such lane claims
+// the group's slots with ONE LDS atomic on the digit cursor -> stable by construction.
+// Segments and the chunk / hot work lists are then built by the same wave with wave scans.
+constexpr int kWaveSortMax = 4096;
+constexpr int kWaveDigitBits = 12;
 
-__global__ __launch_bounds__(256) void indexer_pack_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
-                                                           const void* __restrict__ idx, int itype, int64_t tstride,
-                                                           int base, int N, unsigned* __restrict__ err) {
-    const int t = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= N) return;
-    const int64_t nrows = tabs[t].nrows;
-    const int64_t r = load_index(idx, itype, t * tstride + p) - base;
-    uint32_t key = (uint32_t)nrows;  // sentinel: sorts after every valid row
-    if (r >= 0 && r < nrows) key = (uint32_t)r;
-    else raise_index_error(err);
-    ix.key64[(int64_t)t * ix.cap + p] = ((uint64_t)key << 32) | (uint32_t)p;
-}
-
-__global__ __launch_bounds__(512) void indexer_rank_kernel(IndexerDev ix, int N) {
-    // the table's keys staged once in LDS; every lane then reads them back as 2-key
-    // broadcasts (ds_read_b128, same address in all lanes) with the compares pipelined
-    // behind in-order LDS returns.
-    __shared__ __attribute__((aligned(16))) uint64_t keys[kRankMax + 32];  // +32: ~0 padding for the prefetch
-    const int t = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t off = (int64_t)t * ix.cap;
-    const uint64_t* __restrict__ K = ix.key64 + off;
-    for (int i = threadIdx.x; i < kRankMax + 32; i += blockDim.x) keys[i] = i < N ? K[i] : ~0ull;
-    __syncthreads();
-    const uint64_t kp = p < N ? keys[p] : ~0ull;
-    const int n16 = (N + 15) & ~15;  // padding keys (~0) are never smaller than a real key
-    int c[4] = {0, 0, 0, 0};
-    const ulonglong2* k2 = (const ulonglong2*)keys;
-    // two 8-key batches in flight: batch b+1's LDS reads overlap batch b's compares
-    ulonglong2 va[4], vb[4];
+__device__ __forceinline__ int wave_scan_excl(int v, int lane, int* total) {
+    int x = v;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) va[k] = k2[k];
-    for (int q = 0; q < n16; q += 16) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vb[k] = k2[(q + 8) / 2 + k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] += (va[k].x < kp ? 1 : 0) + (va[k].y < kp ? 1 : 0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) va[k] = k2[(q + 16) / 2 + k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] += (vb[k].x < kp ? 1 : 0) + (vb[k].y < kp ? 1 : 0);
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
     }
-    if (p >= N) return;
-    const int rank = c[0] + c[1] + c[2] + c[3];
-    ix.keys0[off + rank] = (uint32_t)(kp >> 32);
-    ix.vals0[off + rank] = p;
+    *total = __shfl(x, 63, 64);
+    return x - v;
 }
 
-__global__ __launch_bounds__(kBuildThreads) void indexer_segments_kernel(IndexerDev ix,
-                                                                          const TableDesc* __restrict__ tabs, int N) {
-    __shared__ SortLds sl;
+struct WaveLds {
+    uint32_t keys[2][kWaveSortMax];
+    int32_t vals[2][kWaveSortMax];
+    int32_t cursor[1 << kWaveDigitBits];
+};
+
+__global__ __launch_bounds__(64) void indexer_wave_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
+                                                          const void* __restrict__ idx, int itype, int64_t tstride,
+                                                          int base, int N, unsigned* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    WaveLds& sl = *(WaveLds*)dyn;
     const int t = blockIdx.x;
+    const int lane = threadIdx.x;
     const int64_t off = (int64_t)t * ix.cap;
-    build_segments(ix, t, ix.keys0 + off, ix.vals0 + off, N, (uint32_t)tabs[t].nrows, sl);
+    const uint32_t nrows = (uint32_t)tabs[t].nrows;
+    const uint32_t sentinel = nrows;
+    const int nbits = 32 - __clz(nrows);
+    const int passes = nbits <= kWaveDigitBits ? 1 : (nbits + kWaveDigitBits - 1) / kWaveDigitBits;
+    const int dbits_all = (nbits + passes - 1) / passes;
+    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // pass-0 input straight from the index array
+    for (int i = lane; i < N; i += 64) {
+        const int64_t r = load_index(idx, itype, t * tstride + i) - base;
+        uint32_t k = sentinel;
+        if (r >= 0 && r < (int64_t)nrows) k = (uint32_t)r;
+        else raise_index_error(err);
+        sl.keys[0][i] = k;
+        sl.vals[0][i] = i;
+    }
+    int cur = 0;
+    for (int pass = 0; pass < passes; ++pass) {
+        const int shift = pass * dbits_all;
+        const int dbits = nbits - shift < dbits_all ? nbits - shift : dbits_all;
+        const int ndig = 1 << dbits;
+        const uint32_t mask = (uint32_t)ndig - 1u;
+        for (int d = lane; d < ndig; d += 64) sl.cursor[d] = 0;
+        wave_lds_sync();
+        for (int i = lane; i < N; i += 64) atomicAdd(&sl.cursor[(sl.keys[cur][i] >> shift) & mask], 1);
+        wave_lds_sync();
+        // exclusive scan of the cursors, 64 digits per step
+        int carry = 0;
+        for (int d0 = 0; d0 < ndig; d0 += 64) {
+            const int d = d0 + lane;
+            const int c = d < ndig ? sl.cursor[d] : 0;
+            int tot;
+            const int ex = wave_scan_excl(c, lane, &tot);
+            if (d < ndig) sl.cursor[d] = carry + ex;
+            carry += tot;
+        }
+        wave_lds_sync();
+        for (int i0 = 0; i0 < N; i0 += 64) {
+            const int i = i0 + lane;
+            const bool valid = i < N;
+            const uint32_t key = valid ? sl.keys[cur][i] : 0u;
+            const int32_t val = valid ? sl.vals[cur][i] : 0;
+            const uint32_t digit = (key >> shift) & mask;
+            unsigned long long peers = __ballot(valid);
+            for (int bit = 0; bit < dbits; ++bit) {
+                const unsigned long long bb = __ballot(valid && ((digit >> bit) & 1u));
+                peers &= ((digit >> bit) & 1u) ? bb : ~bb;
+            }
+            const int rank = __popcll(peers & lt_mask);
+            const int leader = valid ? __ffsll((long long)peers) - 1 : 0;
+            int b0 = 0;
+            if (valid && rank == 0) b0 = atomicAdd(&sl.cursor[digit], __popcll(peers));
+            b0 = __shfl(b0, leader, 64);
+            if (valid) {
+                sl.keys[cur ^ 1][b0 + rank] = key;
+                sl.vals[cur ^ 1][b0 + rank] = val;
+            }
+        }
+        wave_lds_sync();
+        cur ^= 1;
+    }
+    const uint32_t* K = sl.keys[cur];
+    const int32_t* V = sl.vals[cur];
+    int32_t* lseg = sl.vals[cur ^ 1];   // free after the last pass: segment starts
+    uint32_t* lrow = sl.keys[cur ^ 1];  // and rows, kept in LDS for the chunk pass
+    // segments
+    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+    int32_t* perm = ix.perm + off;
+    int U = 0, nvalid = 0;
+    for (int i0 = 0; i0 < N; i0 += 64) {
+        const int i = i0 + lane;
+        const uint32_t k = i < N ? K[i] : sentinel;
+        const bool live = k != sentinel;
+        const bool head = live && (i == 0 || K[i - 1] != k);
+        if (live) perm[i] = V[i];
+        int tot;
+        const int ex = wave_scan_excl(head ? 1 : 0, lane, &tot);
+        if (head) {
+            seg_start[U + ex] = i;
+            seg_row[U + ex] = k;
+            lseg[U + ex] = i;
+            lrow[U + ex] = k;
+        }
+        U += tot;
+        nvalid += __popcll(__ballot(live));
+    }
+    if (lane == 0) seg_start[U] = nvalid;
+    wave_lds_sync();
+    // chunk and hot-segment work lists
+    int4* chunks = ix.chunks + off;
+    uint32_t* hot_row = ix.hot_row + off;
+    int32_t* hot_slot0 = ix.hot_slot0 + off;
+    int32_t* hot_n = ix.hot_n + off;
+    int C = 0, H = 0, HC = 0;
+    for (int s0 = 0; s0 < U; s0 += 64) {
+        const int s = s0 + lane;
+        int beg = 0, end = 0;
+        if (s < U) { beg = lseg[s]; end = s + 1 < U ? lseg[s + 1] : nvalid; }
+        const int nch = (end - beg + kChunk - 1) / kChunk;
+        const bool hot = nch > 1;
+        int ctot, htot, hctot;
+        const int c0 = wave_scan_excl(nch, lane, &ctot);
+        const int h0 = wave_scan_excl(hot ? 1 : 0, lane, &htot);
+        const int hc0 = wave_scan_excl(hot ? nch : 0, lane, &hctot);
+        if (s < U) {
+            const uint32_t row = lrow[s];
+            for (int k = 0; k < nch; ++k) {
+                const int b0 = beg + k * kChunk;
+                chunks[C + c0 + k] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, hot ? H + h0 : (int)row,
+                                               hot ? HC + hc0 + k : -1);
+            }
+            if (hot) {
+                hot_row[H + h0] = row;
+                hot_slot0[H + h0] = HC + hc0;
+                hot_n[H + h0] = nch;
+                ix.hot_cnt[off + H + h0] = 0;
+            }
+        }
+        C += ctot; H += htot; HC += hctot;
+    }
+    if (lane == 0) {
+        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
+    }
 }
 
 // Row read-modify-write of NE consecutive elements at element offset c0: row -= lr * acc,
@@ -580,15 +677,12 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-    if (N == 0) {
-        hipLaunchKernelGGL(indexer_segments_kernel, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, 0);
-    } else if (N <= kRankMax) {
-        const dim3 grid((unsigned)((N + 255) / 256), T_);
-        hipLaunchKernelGGL(indexer_pack_kernel, grid, dim3(256), 0, s, ix, tabs, idx, itype, tstride, base, (int)N,
-                           ctx_error_word(ctx));
-        // 512-thread blocks: two waves per SIMD hide each other's LDS latency
-        hipLaunchKernelGGL(indexer_rank_kernel, dim3((unsigned)((N + 511) / 512), T_), dim3(512), 0, s, ix, (int)N);
-        hipLaunchKernelGGL(indexer_segments_kernel, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, (int)N);
+    if (N <= kWaveSortMax) {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)indexer_wave_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(WaveLds));
+        if (attr != hipSuccess) return ctx_hip(ctx, attr, "hipFuncSetAttribute(indexer_wave_kernel)");
+        hipLaunchKernelGGL(indexer_wave_kernel, dim3(T_), dim3(64), sizeof(WaveLds), s, ix, tabs, idx, itype, tstride,
+                           base, (int)N, ctx_error_word(ctx));
     } else if (N <= kLdsSortMax)
         hipLaunchKernelGGL(indexer_build_kernel<true>, dim3(T_), dim3(kBuildThreads), indexer_lds_bytes(), s, ix, tabs,
                            idx, itype, tstride, base, B, L, ctx_error_word(ctx));
