@@ -60,13 +60,46 @@ __device__ __forceinline__ int block_scan_excl(int v, int* wtot, int* tot) {
     return before + x - v;
 }
 
+constexpr int kDigits = 257;        // 256 row digits + 1 bucket that keeps invalid indices last
+constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
+
 struct SortLds {
-    int hist[kBuildWaves][256];
-    int cnt[kBuildWaves][256];
-    int digit_off[256];
+    int cnt[kBuildWaves][kDigits + 7];  // per-wave digit counts, then their global offsets
+    int hist[kDigits + 7];
+    int digit_off[kDigits + 7];
+    int bucket_start[kDigits + 8];
     int wtot[2 * kBuildWaves];
+    long long wtot64[2 * kBuildWaves];
     int nvalid;
+    int maxbucket;
 };
+
+// Exclusive scan of a 64-bit value over the 1024 threads (three packed 21-bit counters).
+__device__ __forceinline__ long long block_scan_excl64(long long v, long long* wtot, long long* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        long long t = lane < kBuildWaves ? wtot[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const long long y = __shfl_up(t, off, 64);
+            if (lane >= off) t += y;
+        }
+        if (lane < kBuildWaves) wtot[kBuildWaves + lane] = t;
+    }
+    __syncthreads();
+    const long long before = w ? wtot[kBuildWaves + w - 1] : 0;
+    *tot = wtot[2 * kBuildWaves - 1];
+    __syncthreads();
+    return before + x - v;
+}
 
 // Segments + chunk/hot work lists from a table's sorted (row, position) arrays; one
 // 1024-thread workgroup per table.  K/V may live in LDS or global memory.
@@ -74,8 +107,6 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
                                uint32_t sentinel, SortLds& sl) {
     const int tid = threadIdx.x;
     const int64_t off = (int64_t)t * ix.cap;
-
-    // ---- segments: one per distinct valid row; perm = sorted positions
     if (tid == 0) sl.nvalid = 0;
     __syncthreads();
     int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
@@ -103,43 +134,117 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
     const int nvalid = sl.nvalid;
     if (tid == 0) seg_start[U] = nvalid;
     __syncthreads();
-
-    // ---- chunk and hot-segment work lists
     int4* chunks = ix.chunks + off;
     uint32_t* hot_row = ix.hot_row + off;
     int32_t* hot_slot0 = ix.hot_slot0 + off;
     int32_t* hot_n = ix.hot_n + off;
-    int C = 0, H = 0, HC = 0;
+    long long C = 0, H = 0, HC = 0;
+    constexpr long long M21 = (1ll << 21) - 1;
     for (int tile = 0; tile < U; tile += kBuildThreads) {
         const int s = tile + tid;
         int beg = 0, end = 0;
         if (s < U) { beg = seg_start[s]; end = seg_start[s + 1]; }
         const int nch = (end - beg + kChunk - 1) / kChunk;
         const bool hot = nch > 1;
-        int ctot, htot, hctot;
-        const int c0 = block_scan_excl(nch, sl.wtot, &ctot);
-        const int h0 = block_scan_excl(hot ? 1 : 0, sl.wtot, &htot);
-        const int hc0 = block_scan_excl(hot ? nch : 0, sl.wtot, &hctot);
+        // one scan of three packed counters: chunks | hot segments | hot chunks (each < 2^21 per tile)
+        const long long packed = (long long)nch | ((long long)(hot ? 1 : 0) << 21) | ((long long)(hot ? nch : 0) << 42);
+        long long tot;
+        const long long ex = block_scan_excl64(packed, sl.wtot64, &tot);
+        const long long c0 = ex & M21, h0 = (ex >> 21) & M21, hc0 = (ex >> 42) & M21;
         if (s < U) {
             const uint32_t row = seg_row[s];
             for (int k = 0; k < nch; ++k) {
-                const int cid = C + c0 + k;
+                const int cid = (int)(C + c0 + k);
                 const int b0 = beg + k * kChunk;
-                chunks[cid] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, hot ? H + h0 : (int)row,
-                                        hot ? HC + hc0 + k : -1);
+                chunks[cid] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, hot ? (int)(H + h0) : (int)row,
+                                        hot ? (int)(HC + hc0 + k) : -1);
             }
             if (hot) {
                 hot_row[H + h0] = row;
-                hot_slot0[H + h0] = HC + hc0;
+                hot_slot0[H + h0] = (int)(HC + hc0);
                 hot_n[H + h0] = nch;
                 ix.hot_cnt[off + H + h0] = 0;  // arrival counter, reset every build
             }
         }
-        C += ctot; H += htot; HC += hctot;
+        C += tot & M21; H += (tot >> 21) & M21; HC += (tot >> 42) & M21;
     }
     if (tid == 0) {
         int32_t* cnt = ix.counts + (int64_t)t * 8;
-        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
+        cnt[CNT_U] = U; cnt[CNT_C] = (int)C; cnt[CNT_H] = (int)H; cnt[CNT_HC] = (int)HC; cnt[CNT_NV] = nvalid;
+    }
+}
+
+// One stable counting-sort pass of (key, val) by digit(key); digit 256 = invalid index.
+// Tiles of 1024 positions in order; per wave the lanes sharing a digit are found with
+// 9 ballots (multi-split), the cross-wave offsets go through LDS.
+template <typename GetKV>
+__device__ void radix_pass(int N, int shift, bool first_pass, uint32_t sentinel, GetKV get, uint32_t* kout,
+                           int32_t* vout, SortLds& sl) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int d = tid; d < kDigits; d += kBuildThreads) sl.hist[d] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += kBuildThreads) {
+        uint32_t key;
+        int32_t val;
+        get(i, key, val);
+        atomicAdd(&sl.hist[key == sentinel ? 256 : (key >> shift) & 255u], 1);
+    }
+    __syncthreads();
+    {
+        const int v = tid < kDigits ? sl.hist[tid] : 0;
+        int tot;
+        const int ex = block_scan_excl(v, sl.wtot, &tot);
+        if (tid < kDigits) {
+            sl.digit_off[tid] = ex;
+            if (first_pass) sl.bucket_start[tid] = ex;
+        }
+        if (first_pass && tid == 0) sl.bucket_start[kDigits] = N;
+        if (first_pass) {
+            // largest valid-row bucket (decides rank sort vs more radix passes)
+            int m = tid < 256 ? v : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+            if (tid == 0) sl.maxbucket = 0;
+            __syncthreads();
+            if (lane == 0 && m > 0) atomicMax(&sl.maxbucket, m);
+        }
+        __syncthreads();
+    }
+    for (int tile = 0; tile < N; tile += kBuildThreads) {
+        const int i = tile + tid;
+        const bool valid = i < N;
+        uint32_t key = 0;
+        int32_t val = 0;
+        if (valid) get(i, key, val);
+        const uint32_t digit = key == sentinel ? 256u : (key >> shift) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 9; ++bit) {
+            const unsigned long long bb = __ballot(valid && ((digit >> bit) & 1u));
+            peers &= ((digit >> bit) & 1u) ? bb : ~bb;
+        }
+        const int rank = __popcll(peers & lt_mask);
+        for (int e = lane; e < kDigits; e += 64) sl.cnt[w][e] = 0;
+        __syncthreads();
+        if (valid && rank == 0) sl.cnt[w][digit] = __popcll(peers);
+        __syncthreads();
+        if (tid < kDigits) {
+            int run = sl.digit_off[tid];
+            for (int ww = 0; ww < kBuildWaves; ++ww) {
+                const int c = sl.cnt[ww][tid];
+                sl.cnt[ww][tid] = run;
+                run += c;
+            }
+            sl.digit_off[tid] = run;
+        }
+        __syncthreads();
+        if (valid) {
+            const int dst = sl.cnt[w][digit] + rank;
+            kout[dst] = key;
+            vout[dst] = val;
+        }
+        __syncthreads();
     }
 }
 
@@ -150,14 +255,12 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     __shared__ SortLds sl;
     const int t = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x;
     const int N = B * L;
     const int64_t off = (int64_t)t * ix.cap;
     const uint32_t nrows = (uint32_t)tabs[t].nrows;  // host checks nrows < 2^32 - 1
     const uint32_t sentinel = nrows;
-    const int nbits = 32 - __clz(nrows);             // bits of the sentinel value
-    const int passes = nbits == 0 ? 1 : (nbits + 7) / 8;
-
+    const int nbits = 32 - __clz(nrows > 0 ? nrows - 1 : 0);  // bits of the largest valid row
     uint32_t* kbuf[2];
     int32_t* vbuf[2];
     if (IN_LDS) {
@@ -169,248 +272,55 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
         kbuf[0] = ix.keys0 + off; kbuf[1] = ix.keys1 + off;
         vbuf[0] = ix.vals0 + off; vbuf[1] = ix.vals1 + off;
     }
-    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-
-    for (int pass = 0; pass < passes; ++pass) {
-        const int shift = 8 * pass;
-        const int dbits = nbits - shift < 8 ? (nbits - shift > 0 ? nbits - shift : 0) : 8;
-        const uint32_t mask = (1u << dbits) - 1u;
-        const uint32_t* kin = kbuf[pass & 1];
-        const int32_t* vin = vbuf[pass & 1];
-        uint32_t* kout = kbuf[(pass + 1) & 1];
-        int32_t* vout = vbuf[(pass + 1) & 1];
-
-        for (int e = tid; e < kBuildWaves * 256; e += kBuildThreads) (&sl.hist[0][0])[e] = 0;
-        __syncthreads();
-        // histogram; pass 0 reads the raw indices and validates them
-        for (int i = tid; i < N; i += kBuildThreads) {
-            uint32_t key;
-            if (pass == 0) {
-                const int64_t r = load_index(idx, itype, t * tstride + i) - base;
-                if (r >= 0 && r < (int64_t)nrows) key = (uint32_t)r;
-                else { key = sentinel; raise_index_error(err); }
-            } else {
-                key = kin[i];
-            }
-            atomicAdd(&sl.hist[w][(key >> shift) & mask], 1);
-        }
-        __syncthreads();
-        {
-            int tot = 0;
-            int v = 0;
-            if (tid < 256) for (int ww = 0; ww < kBuildWaves; ++ww) v += sl.hist[ww][tid];
-            const int ex = block_scan_excl(tid < 256 ? v : 0, sl.wtot, &tot);
-            if (tid < 256) sl.digit_off[tid] = ex;
-            __syncthreads();
-        }
-        // stable scatter, one 1024-element tile at a time in position order
-        for (int tile = 0; tile < N; tile += kBuildThreads) {
-            const int i = tile + tid;
-            const bool valid = i < N;
-            uint32_t key = 0;
-            int32_t val = 0;
-            if (valid) {
-                if (pass == 0) {
-                    const int64_t r = load_index(idx, itype, t * tstride + i) - base;
-                    key = (r >= 0 && r < (int64_t)nrows) ? (uint32_t)r : sentinel;
-                    val = i;
-                } else {
-                    key = kin[i];
-                    val = vin[i];
-                }
-            }
-            const uint32_t digit = (key >> shift) & mask;
-            unsigned long long peers = __ballot(valid);
-            for (int bit = 0; bit < dbits; ++bit) {
-                const unsigned long long bb = __ballot(valid && ((digit >> bit) & 1u));
-                peers &= ((digit >> bit) & 1u) ? bb : ~bb;
-            }
-            const int rank = __popcll(peers & lt_mask);
-            for (int e = lane; e < 256; e += 64) sl.cnt[w][e] = 0;
-            __syncthreads();
-            if (valid && rank == 0) sl.cnt[w][digit] = __popcll(peers);
-            __syncthreads();
-            if (tid < 256) {
-                int run = sl.digit_off[tid];
-                for (int ww = 0; ww < kBuildWaves; ++ww) {
-                    const int c = sl.cnt[ww][tid];
-                    sl.cnt[ww][tid] = run;
-                    run += c;
-                }
-                sl.digit_off[tid] = run;
-            }
-            __syncthreads();
-            if (valid) {
-                const int dst = sl.cnt[w][digit] + rank;
-                kout[dst] = key;
-                vout[dst] = val;
-            }
-            __syncthreads();
-        }
-    }
-    build_segments(ix, t, kbuf[passes & 1], vbuf[passes & 1], N, sentinel, sl);
-}
-
-
-// ---- single-wave indexer (N <= kWaveSortMax): one 64-lane wave per table, no workgroup
-// barriers.  LSD radix over ceil(nbits/12) passes (two passes for the 24-bit Kaggle rows, one
-// for every table under 4096 rows).  Each pass: LDS histogram, wave-level exclusive scan of
-// the digit cursors, then the positions in order, 64 at a time: a lane finds the lanes with
-// its digit by ballots (multi-split), its rank among them, and the lowest such lane claims
-// the group's slots with ONE LDS atomic on the digit cursor -> stable by construction.
-// Segments and the chunk / hot work lists are then built by the same wave with wave scans.
-constexpr int kWaveSortMax = 4096;
-constexpr int kWaveDigitBits = 12;
-
-__device__ __forceinline__ int wave_scan_excl(int v, int lane, int* total) {
-    int x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    *total = __shfl(x, 63, 64);
-    return x - v;
-}
-
-struct WaveLds {
-    uint32_t keys[2][kWaveSortMax];
-    int32_t vals[2][kWaveSortMax];
-    int32_t cursor[1 << kWaveDigitBits];
-};
-
-__global__ __launch_bounds__(64) void indexer_wave_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
-                                                          const void* __restrict__ idx, int itype, int64_t tstride,
-                                                          int base, int N, unsigned* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    WaveLds& sl = *(WaveLds*)dyn;
-    const int t = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int64_t off = (int64_t)t * ix.cap;
-    const uint32_t nrows = (uint32_t)tabs[t].nrows;
-    const uint32_t sentinel = nrows;
-    const int nbits = 32 - __clz(nrows);
-    const int passes = nbits <= kWaveDigitBits ? 1 : (nbits + kWaveDigitBits - 1) / kWaveDigitBits;
-    const int dbits_all = (nbits + passes - 1) / passes;
-    const unsigned long long lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-    // pass-0 input straight from the index array
-    for (int i = lane; i < N; i += 64) {
+    // pass 0 straight from the index array (validated here)
+    auto get0 = [&](int i, uint32_t& key, int32_t& val) {
         const int64_t r = load_index(idx, itype, t * tstride + i) - base;
-        uint32_t k = sentinel;
-        if (r >= 0 && r < (int64_t)nrows) k = (uint32_t)r;
-        else raise_index_error(err);
-        sl.keys[0][i] = k;
-        sl.vals[0][i] = i;
+        key = (r >= 0 && r < (int64_t)nrows) ? (uint32_t)r : sentinel;
+        val = i;
+    };
+    for (int i = tid; i < N; i += kBuildThreads) {  // report invalid indices once
+        uint32_t k;
+        int32_t v;
+        get0(i, k, v);
+        if (k == sentinel) raise_index_error(err);
     }
-    int cur = 0;
-    for (int pass = 0; pass < passes; ++pass) {
-        const int shift = pass * dbits_all;
-        const int dbits = nbits - shift < dbits_all ? nbits - shift : dbits_all;
-        const int ndig = 1 << dbits;
-        const uint32_t mask = (uint32_t)ndig - 1u;
-        for (int d = lane; d < ndig; d += 64) sl.cursor[d] = 0;
-        wave_lds_sync();
-        for (int i = lane; i < N; i += 64) atomicAdd(&sl.cursor[(sl.keys[cur][i] >> shift) & mask], 1);
-        wave_lds_sync();
-        // exclusive scan of the cursors, 64 digits per step
-        int carry = 0;
-        for (int d0 = 0; d0 < ndig; d0 += 64) {
-            const int d = d0 + lane;
-            const int c = d < ndig ? sl.cursor[d] : 0;
-            int tot;
-            const int ex = wave_scan_excl(c, lane, &tot);
-            if (d < ndig) sl.cursor[d] = carry + ex;
-            carry += tot;
-        }
-        wave_lds_sync();
-        for (int i0 = 0; i0 < N; i0 += 64) {
-            const int i = i0 + lane;
-            const bool valid = i < N;
-            const uint32_t key = valid ? sl.keys[cur][i] : 0u;
-            const int32_t val = valid ? sl.vals[cur][i] : 0;
-            const uint32_t digit = (key >> shift) & mask;
-            unsigned long long peers = __ballot(valid);
-            for (int bit = 0; bit < dbits; ++bit) {
-                const unsigned long long bb = __ballot(valid && ((digit >> bit) & 1u));
-                peers &= ((digit >> bit) & 1u) ? bb : ~bb;
+    radix_pass(N, 0, true, sentinel, get0, kbuf[1], vbuf[1], sl);
+    int cur = 1;
+    if (nbits > 8) {
+        if (sl.maxbucket <= kRankBucketMax) {
+            // every low-byte bucket is small: order each bucket by (row, position) directly.
+            // Stable pass 0 left each bucket in position order, so j < i <=> pos_j < pos_i.
+            for (int i = tid; i < N; i += kBuildThreads) {
+                const uint32_t ki = kbuf[1][i];
+                if (ki == sentinel) {  // invalid indices stay in the last bucket, in order
+                    kbuf[0][i] = ki;
+                    vbuf[0][i] = vbuf[1][i];
+                    continue;
+                }
+                const int d = ki & 255u;
+                const int bs = sl.bucket_start[d], be = sl.bucket_start[d + 1];
+                int rank = 0;
+                for (int j = bs; j < be; ++j) {
+                    const uint32_t kj = kbuf[1][j];
+                    rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+                }
+                kbuf[0][bs + rank] = ki;
+                vbuf[0][bs + rank] = vbuf[1][i];
             }
-            const int rank = __popcll(peers & lt_mask);
-            const int leader = valid ? __ffsll((long long)peers) - 1 : 0;
-            int b0 = 0;
-            if (valid && rank == 0) b0 = atomicAdd(&sl.cursor[digit], __popcll(peers));
-            b0 = __shfl(b0, leader, 64);
-            if (valid) {
-                sl.keys[cur ^ 1][b0 + rank] = key;
-                sl.vals[cur ^ 1][b0 + rank] = val;
+            __syncthreads();
+            cur = 0;
+        } else {
+            // skewed rows: remaining LSD passes (invalid indices keep digit 256 -> stay last)
+            for (int shift = 8; shift < nbits; shift += 8) {
+                const uint32_t* kin = kbuf[cur];
+                const int32_t* vin = vbuf[cur];
+                auto get = [&](int i, uint32_t& key, int32_t& val) { key = kin[i]; val = vin[i]; };
+                radix_pass(N, shift, false, sentinel, get, kbuf[cur ^ 1], vbuf[cur ^ 1], sl);
+                cur ^= 1;
             }
         }
-        wave_lds_sync();
-        cur ^= 1;
     }
-    const uint32_t* K = sl.keys[cur];
-    const int32_t* V = sl.vals[cur];
-    int32_t* lseg = sl.vals[cur ^ 1];   // free after the last pass: segment starts
-    uint32_t* lrow = sl.keys[cur ^ 1];  // and rows, kept in LDS for the chunk pass
-    // segments
-    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
-    uint32_t* seg_row = ix.seg_row + off;
-    int32_t* perm = ix.perm + off;
-    int U = 0, nvalid = 0;
-    for (int i0 = 0; i0 < N; i0 += 64) {
-        const int i = i0 + lane;
-        const uint32_t k = i < N ? K[i] : sentinel;
-        const bool live = k != sentinel;
-        const bool head = live && (i == 0 || K[i - 1] != k);
-        if (live) perm[i] = V[i];
-        int tot;
-        const int ex = wave_scan_excl(head ? 1 : 0, lane, &tot);
-        if (head) {
-            seg_start[U + ex] = i;
-            seg_row[U + ex] = k;
-            lseg[U + ex] = i;
-            lrow[U + ex] = k;
-        }
-        U += tot;
-        nvalid += __popcll(__ballot(live));
-    }
-    if (lane == 0) seg_start[U] = nvalid;
-    wave_lds_sync();
-    // chunk and hot-segment work lists
-    int4* chunks = ix.chunks + off;
-    uint32_t* hot_row = ix.hot_row + off;
-    int32_t* hot_slot0 = ix.hot_slot0 + off;
-    int32_t* hot_n = ix.hot_n + off;
-    int C = 0, H = 0, HC = 0;
-    for (int s0 = 0; s0 < U; s0 += 64) {
-        const int s = s0 + lane;
-        int beg = 0, end = 0;
-        if (s < U) { beg = lseg[s]; end = s + 1 < U ? lseg[s + 1] : nvalid; }
-        const int nch = (end - beg + kChunk - 1) / kChunk;
-        const bool hot = nch > 1;
-        int ctot, htot, hctot;
-        const int c0 = wave_scan_excl(nch, lane, &ctot);
-        const int h0 = wave_scan_excl(hot ? 1 : 0, lane, &htot);
-        const int hc0 = wave_scan_excl(hot ? nch : 0, lane, &hctot);
-        if (s < U) {
-            const uint32_t row = lrow[s];
-            for (int k = 0; k < nch; ++k) {
-                const int b0 = beg + k * kChunk;
-                chunks[C + c0 + k] = make_int4(b0, b0 + kChunk < end ? b0 + kChunk : end, hot ? H + h0 : (int)row,
-                                               hot ? HC + hc0 + k : -1);
-            }
-            if (hot) {
-                hot_row[H + h0] = row;
-                hot_slot0[H + h0] = HC + hc0;
-                hot_n[H + h0] = nch;
-                ix.hot_cnt[off + H + h0] = 0;
-            }
-        }
-        C += ctot; H += htot; HC += hctot;
-    }
-    if (lane == 0) {
-        int32_t* cnt = ix.counts + (int64_t)t * 8;
-        cnt[CNT_U] = U; cnt[CNT_C] = C; cnt[CNT_H] = H; cnt[CNT_HC] = HC; cnt[CNT_NV] = nvalid;
-    }
+    build_segments(ix, t, kbuf[cur], vbuf[cur], N, sentinel, sl);
 }
 
 // Row read-modify-write of NE consecutive elements at element offset c0: row -= lr * acc,
@@ -677,13 +587,7 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-    if (N <= kWaveSortMax) {
-        static const hipError_t attr = hipFuncSetAttribute((const void*)indexer_wave_kernel,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(WaveLds));
-        if (attr != hipSuccess) return ctx_hip(ctx, attr, "hipFuncSetAttribute(indexer_wave_kernel)");
-        hipLaunchKernelGGL(indexer_wave_kernel, dim3(T_), dim3(64), sizeof(WaveLds), s, ix, tabs, idx, itype, tstride,
-                           base, (int)N, ctx_error_word(ctx));
-    } else if (N <= kLdsSortMax)
+    if (N <= kLdsSortMax)
         hipLaunchKernelGGL(indexer_build_kernel<true>, dim3(T_), dim3(kBuildThreads), indexer_lds_bytes(), s, ix, tabs,
                            idx, itype, tstride, base, B, L, ctx_error_word(ctx));
     else

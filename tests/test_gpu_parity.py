@@ -203,11 +203,15 @@ def _np_segments(idx_row):
     return rows, order
 
 
-@pytest.mark.parametrize("rows,B,L", [([3, 4, 10, 1000, 5_000_000], 2048, 1), ([1000, 7, 20000], 300, 10),
-                                      ([2], 1, 1), ([100000, 3], 5000, 1)])
-def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L):
+@pytest.mark.parametrize("rows,B,L,zipf", [([3, 4, 10, 1000, 5_000_000], 2048, 1, None), ([1000, 7, 20000], 300, 10, None),
+                                           ([2], 1, 1, None), ([100000, 3], 5000, 1, None), ([256, 257, 70000], 2048, 1, None),
+                                           ([300, 100000, 5_000_000], 2048, 1, 1.1), ([100000, 1000], 4000, 2, 1.2),
+                                           ([0x10000, 0x1000000], 1500, 1, None)])
+def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
+    """Both sort strategies (1 pass + bucket rank; full LSD radix on skewed rows), LDS and
+    global-scratch variants: unique rows and per-row positions must match numpy exactly."""
     rng = np.random.default_rng(B + L)
-    idx = rand_indices(rng, rows, B, L)
+    idx = rand_indices(rng, rows, B, L, zipf=zipf)
     tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B * L, gpu)
     ix.build(tabs, torch.from_numpy(idx).reshape(len(rows), B, L).to(gpu), index_base=0)
