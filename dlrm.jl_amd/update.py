@@ -94,7 +94,7 @@ class SparseIndexer:
         return self
 
     def unique_rows(self, table):
-        """Sorted 0-based unique rows touched in `table` by the last build (synchronises)."""
+        """0-based unique rows touched in `table` by the last build, in segment order (synchronises)."""
         n = ctypes.c_int64()
         cap = self.capacity
         rows = (ctypes.c_int64 * max(cap, 1))()
@@ -103,7 +103,8 @@ class SparseIndexer:
         return list(rows[: n.value])
 
     def segments(self, table):
-        """(unique_rows, positions, seg_start) of `table`: positions sorted by row, ascending within a row."""
+        """(unique_rows, positions, seg_start) of `table`: positions grouped by row (one segment per
+        row, segment order unspecified), ascending within a row."""
         n = ctypes.c_int64()
         cap = self.capacity
         rows = (ctypes.c_int64 * max(cap, 1))()

@@ -141,14 +141,15 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_table,
                         dlrm_indexer** out);
 int dlrm_indexer_destroy(dlrm_indexer* indexer);
-/* Dedupe: per table, a stable sort of positions by row -> unique rows + the positions that
- * hit each of them in ascending order.  Asynchronous; device-side counts only. */
+/* Dedupe: per table, group the lookup positions by row -> one segment per distinct row
+ * holding the positions that hit it in ascending order (segment order is unspecified).
+ * Asynchronous; device-side counts only. */
 int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
                        const void* indices, int itype, int64_t table_stride, int index_base,
                        int batch, int lookups);
 /* Inspection (synchronous): unique-row count of one table; if rows != NULL copies up to
- * cap unique rows (0-based, ascending); if positions != NULL copies up to cap sorted
- * positions (b*lookups + k) and their segment starts (cap+1 entries) into seg_start. */
+ * cap unique rows (0-based, in segment order); if positions != NULL copies up to cap
+ * positions (b*lookups + k) grouped by segment and the segment starts (cap+1 entries). */
 int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
                       int64_t* num_unique, int64_t* rows, int64_t* positions,
                       int64_t* seg_start, int64_t cap);
