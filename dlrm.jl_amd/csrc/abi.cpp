@@ -2,8 +2,7 @@
 //
 // Owns the three handle types (ctx, tables, indexer), validates arguments on the host,
 // maps HIP errors to dlrm_status codes and forwards to the kernel launchers.  No launching
-// entry point allocates or synchronises (hipGraph-capturable); the one exception is the
-// first dlrm_sgd_update on an indexer, which sizes its partial-sum scratch once.
+// entry point allocates or synchronises (hipGraph-capturable).
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -37,8 +36,6 @@ struct dlrm_indexer {
     int T = 0;
     IndexerDev dev{};
     void* block = nullptr;  // one allocation for every array
-    float* partial = nullptr;
-    size_t partial_bytes = 0;
     // recorded by the last build
     bool built = false;
     const void* indices = nullptr;
@@ -290,16 +287,14 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
     const int64_t T = num_tables > 0 ? num_tables : 1;
     ix->dev.cap = cap;
-    ix->dev.hot_cap = cap / 16 + 2;  // sum over hot segments of ceil(len/32) <= 2*N/32
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
     const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1));
     Piece pieces[] = {
         {(void**)&ix->dev.keys0, n * 4},     {(void**)&ix->dev.keys1, n * 4},   {(void**)&ix->dev.vals0, n * 4},
         {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
-        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot_row, n * 4},
-        {(void**)&ix->dev.hot_slot0, n * 4}, {(void**)&ix->dev.hot_n, n * 4},  {(void**)&ix->dev.counts, (size_t)T * 32},
-        {(void**)&ix->dev.hot_cnt, n * 4},
+        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot, n * 16},
+        {(void**)&ix->dev.counts, (size_t)T * 32},
     };
     size_t total = 0;
     for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
@@ -323,7 +318,6 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
 int dlrm_indexer_destroy(dlrm_indexer* ix) {
     if (!ix) return DLRM_OK;
     if (ix->block) (void)hipFree(ix->block);
-    if (ix->partial) (void)hipFree(ix->partial);
     delete ix;
     return DLRM_OK;
 }
@@ -406,17 +400,8 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned f
         rc = dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, lookups);
         if (rc) return rc;
     }
-    const size_t need = sizeof(float) * (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.hot_cap * (size_t)tb->D;
-    if (ix->partial_bytes < need) {  // sized once per (indexer, dim)
-        if (ix->partial) (void)hipFree(ix->partial);
-        ix->partial = nullptr;
-        ix->partial_bytes = 0;
-        rc = ctx_hip(ctx, hipMalloc((void**)&ix->partial, need), "hipMalloc(partial)");
-        if (rc) return rc;
-        ix->partial_bytes = need;
-    }
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
-                            (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr, ix->partial);
+                            (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr);
 }
 
 }  // extern "C"

@@ -82,15 +82,13 @@ namespace dlrm {
 struct IndexerDev {
     uint32_t* keys0;  uint32_t* keys1;   // global sort scratch (cap > kLdsSortMax)
     int32_t* vals0;   int32_t* vals1;
-    int32_t* perm;         // sorted positions (valid prefix)
+    int32_t* perm;         // positions grouped by row, ascending within a row
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
-    int4* chunks;          // {beg, end, row, -1} single-chunk segment | {beg, end, hot id, slot} hot chunk
-    uint32_t* hot_row; int32_t* hot_slot0; int32_t* hot_n;
-    int32_t* hot_cnt;      // per hot segment arrival counter (zeroed by the build, reset by the last arriver)
-    int32_t* counts;       // [T][8]: U, chunks, hot, hot_chunks, nvalid
+    int4* chunks;          // segments of <= kChunk positions: {beg, end, row, 0}
+    int4* hot;             // longer segments: {beg, end, row, 0}, one workgroup each
+    int32_t* counts;       // [T][8]: U, chunks, hot, -, nvalid
     int64_t cap;
-    int64_t hot_cap;       // hot-chunk slots per table
 };
 
 }  // namespace dlrm
@@ -119,7 +117,7 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
                          int itype, int64_t tstride, int base, int B, int L);
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
-                     float lr, float* partial);
+                     float lr);
 int launch_sgd_atomic(dlrm_ctx* ctx, TableDesc* tabs, int T, int D, const void* idx, int itype, int64_t tstride,
                       int base, int B, int L, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
                       float lr);
