@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
-    ap.add_argument("--overlap-indexer", type=int, default=1)
+    ap.add_argument("--overlap-indexer", type=int, default=0)
     ap.add_argument("--fused", type=int, default=1)
     return ap.parse_args()
 

@@ -85,7 +85,7 @@ struct IndexerDev {
     int32_t* perm;         // positions grouped by row, ascending within a row
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
-    int4* chunks;          // segments of <= kChunk positions: {beg, end, row, 0}
+    int4* chunks;          // segments of <= kChunk positions: {beg, end, row, first position}
     int4* hot;             // longer segments: {beg, end, row, 0}, one workgroup each
     int32_t* counts;       // [T][8]: U, chunks, hot, -, nvalid
     int64_t cap;

@@ -197,7 +197,7 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
         const bool ish = s < U && end - beg > kChunk;
         long long tot;
         const long long ex = block_scan_excl<long long>((isc ? 1ll : 0ll) | ((ish ? 1ll : 0ll) << 32), sl.wtot64, &tot);
-        if (isc) chunks[C + (ex & 0xffffffffll)] = make_int4(beg, end, (int)srow[s], 0);
+        if (isc) chunks[C + (ex & 0xffffffffll)] = make_int4(beg, end, (int)srow[s], V[beg]);
         if (ish) hot[H + (ex >> 32)] = make_int4(beg, end, (int)srow[s], 0);
         C += tot & 0xffffffffll;
         H += tot >> 32;
@@ -318,17 +318,20 @@ struct ApplyGeom {
 };
 
 // Sums the grad rows of positions [beg, end) in ascending order into acc (8 rows in flight).
+// first >= 0 is perm[beg] when the caller already has it (saves one dependent load).
 template <typename GT, int VPR>
 __device__ __forceinline__ void sum_positions(const int32_t* __restrict__ perm, int beg, int end, int L,
                                               const GT* __restrict__ gbase, int64_t grad_ld, int v,
-                                              float (&acc)[ApplyGeom<GT, VPR>::VPL][ApplyGeom<GT, VPR>::NE]) {
+                                              float (&acc)[ApplyGeom<GT, VPR>::VPL][ApplyGeom<GT, VPR>::NE],
+                                              int first = -1) {
     typedef ApplyGeom<GT, VPR> G;
     typedef typename G::GV GV;
     constexpr int U = 8;
     for (int i = beg; i < end; i += U) {
         int32_t p[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) p[u] = (i + u < end) ? perm[i + u] : -1;
+        for (int u = 0; u < U; ++u)
+            p[u] = (u == 0 && i == beg && first >= 0) ? first : ((i + u < end) ? perm[i + u] : -1);
         typename GV::type gv[U][G::VPL];
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
         for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
             for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-        sum_positions<GT, VPR>(perm, cd.x, cd.y, L, gbase, grad_ld, v, acc);
+        sum_positions<GT, VPR>(perm, cd.x, cd.y, L, gbase, grad_ld, v, acc, cd.w);
 #pragma unroll
         for (int j = 0; j < G::VPL; ++j) {
 #pragma unroll

@@ -24,7 +24,7 @@ STAGES = [  # (regex on the kernel name, stage)
     (r"interact_bwd", "interact_bwd"),
     (r"maplookup_", "lookup"),
     (r"indexer_build_kernel", "indexer_build"),
-    (r"sgd_chunks", "sgd_update"),
+    (r"sgd_apply|sgd_chunks", "sgd_update"),
     (r"sgd_hot", "sgd_update"),
     (r"sgd_atomic", "sgd_update"),
 ]
