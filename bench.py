@@ -167,9 +167,10 @@ def main():
         def step(k):
             engine.step(x, packs[k % NBATCH], dout)
     else:
-        from dlrm_jl_amd.sharded import ShardedHotPath
-        engine = ShardedHotPath(pkg, w, B, dev, rank, world, lr=a.lr)
-        step = engine.step
+        from dlrm_jl_amd.sharded import make_bench_engine
+        engine, step = make_bench_engine(pkg, w, B, dev, rank, world, a.lr)
+        if a.mode == "graph":
+            a.mode = "eager"  # collectives are launched eagerly (RCCL inside hipGraph capture: not relied on)
 
     # warm-up (also validates indices once)
     for k in range(max(a.warmup, 1)):
@@ -177,6 +178,8 @@ def main():
     torch.cuda.synchronize()
     if world == 1:
         engine.check_bounds()
+    elif engine.ops is not None:
+        engine.ops.ctx.check_bounds()
 
     graphs = None
     if a.mode == "graph":
@@ -279,7 +282,7 @@ def main():
             "data": "synthetic (uniform indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)",
             "config": {"workload": a.workload, "tables": T, "dim": D, "batch_per_gpu": B, "global_batch": B * world,
                        "lookups": L, "index_dtype": "int32", "table_rows": "Criteo-Kaggle (criteo.jl:350-377)",
-                       "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + all-to-all",
+                       "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + RCCL all-to-all",
                        "launch": "hipGraph replay" if graphs is not None else "eager"},
             "roofline": roofline, "cpu_baseline": cpu,
         }

@@ -1,0 +1,124 @@
+"""Table-sharded multi-rank path (dlrm.jl_amd/sharded.py) on CPU: world_size 2 and 3, gloo.
+
+The exchange logic (partition, uneven all-to-all splits, column scatter/gather) is the
+product code; local compute is supplied by the CPU oracle (test-only ShardOps), and the
+result must equal — bit for bit — one process running the same step on the global batch.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class OracleShardOps:
+    """CPU checker with the ShardOps interface (tables: list of numpy arrays)."""
+
+    def __init__(self, tables, lr):
+        import oracle
+        self.o = oracle
+        self.tables = tables
+        self.lr = lr
+
+    def lookup(self, idx, send):
+        self.o.maplookup(self.tables, idx.data.numpy().astype(np.int64), 0, idx.B, idx.L, send.numpy(), 0)
+
+    def interact_fwd(self, x, ys, out, padding):
+        d = x.shape[1]
+        res = self.o.interact_fwd(x.numpy(), ys.numpy(), ys.shape[1] // d, padding)
+        out.copy_(torch.from_numpy(res))
+
+    def interact_bwd(self, dout, ys, dx, dt, padding):
+        d = dx.shape[1]
+        rdx, rdt = self.o.interact_bwd(dout.numpy(), ys.numpy(), d, ys.shape[1] // d, padding)
+        dx.copy_(torch.from_numpy(rdx))
+        dt.copy_(torch.from_numpy(rdt))
+
+    def update(self, idx, grad):
+        self.o.sgd_update(self.tables, idx.data.numpy().astype(np.int64), 0, idx.B, idx.L, grad.numpy(), 0, self.lr)
+
+
+def _problem(T, rows, D, B, world, L, seed=3):
+    rng = np.random.default_rng(seed)
+    tables = [rng.uniform(-1, 1, size=(rows[t], D)).astype(np.float32) for t in range(T)]
+    Bg = B * world
+    idx = np.stack([rng.integers(0, rows[t], size=Bg * L) for t in range(T)]).astype(np.int64)
+    x = rng.standard_normal((Bg, D)).astype(np.float32)
+    F = T + 1
+    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
+    return tables, idx, x, dout
+
+
+def _worker(rank, world, port, cfg, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import ShardedHotPath, TablePartition
+    T, rows, D, B, L, lr = cfg
+    tables, idx, x, dout = _problem(T, rows, D, B, world, L)
+    part = TablePartition(T, world)
+    t0, t1 = part.range(rank)
+    ops = OracleShardOps([tables[t].copy() for t in range(t0, t1)], lr)
+    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, torch.device("cpu"))
+    p = pkg.PackedIndices(torch.from_numpy(idx[t0:t1]).reshape(t1 - t0, B * world, L))
+    sl = slice(rank * B, (rank + 1) * B)
+    eng.step(torch.from_numpy(x[sl]).contiguous(), p, torch.from_numpy(dout[sl]).contiguous())
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), out=eng.out.numpy(), dx=eng.dx.numpy(),
+             **{f"table{t}": ops.tables[t - t0] for t in range(t0, t1)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,T,L", [(2, 5, 1), (2, 7, 3), (3, 4, 1), (3, 2, 2)])
+def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L):
+    import oracle
+    rows = [3, 50, 1000, 7, 400, 12, 90][:T]
+    D, B, lr = 16, 4, 0.5
+    cfg = (T, rows, D, B, L, lr)
+    mp.start_processes(_worker, args=(world, _free_port(), cfg, str(tmp_path)), nprocs=world, start_method="spawn")
+    # single process on the global batch
+    tables, idx, x, dout = _problem(T, rows, D, B, world, L)
+    Bg = B * world
+    F = T + 1
+    ys = np.zeros((Bg, F * D), dtype=np.float32)
+    oracle.maplookup(tables, idx, 0, Bg, L, ys, D)
+    out = oracle.interact_fwd(x, ys, F)
+    dx, dt = oracle.interact_bwd(dout, ys, D, F)
+    oracle.sgd_update(tables, idx, 0, Bg, L, dt, D, lr)
+    from dlrm_jl_amd.sharded import TablePartition
+    part = TablePartition(T, world)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        sl = slice(r * B, (r + 1) * B)
+        assert np.array_equal(z["out"], out[sl])
+        assert np.array_equal(z["dx"], dx[sl])
+        t0, t1 = part.range(r)
+        for t in range(t0, t1):
+            assert np.array_equal(z[f"table{t}"], tables[t]), (r, t)
+
+
+def test_table_partition_is_balanced_and_contiguous():
+    import dlrm_pkg
+    dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import TablePartition
+    for T, W in [(26, 8), (26, 4), (26, 2), (26, 1), (3, 8), (64, 8)]:
+        p = TablePartition(T, W)
+        assert sum(p.counts) == T and max(p.counts) - min(p.counts) <= 1
+        covered = [t for r in range(W) for t in range(*p.range(r))]
+        assert covered == list(range(T))
