@@ -141,10 +141,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))  # one rank per GPU on a full node
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("DLRM_DIST_BACKEND", "nccl")  # "gloo" only for 1-GPU rehearsals
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     w = dict(pkg.WORKLOADS[a.workload])
     B, D, L = w["batch"], w["dim"], w["lookups"]
     rows = w["rows"]

@@ -113,9 +113,19 @@ class ShardedHotPath:
         self.offsets = [sum(self.fwd_out_splits[:j]) for j in range(self.world)]
 
     # ---- exchange (pure data movement; identical for every ShardOps)
+    def _a2a(self, out, inp, out_splits, in_splits):
+        if out.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo has no device all-to-all: stage through host memory (tests / 1-GPU rehearsals;
+            # the product backend is "nccl" = RCCL, which moves device memory over xGMI)
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
     def exchange_fwd(self):
-        dist.all_to_all_single(self.recv, self.send.reshape(-1)[: self.Bg * self.Tr * self.D], self.fwd_out_splits,
-                               self.fwd_in_splits, group=self.group)
+        self._a2a(self.recv, self.send.reshape(-1)[: self.Bg * self.Tr * self.D], self.fwd_out_splits,
+                  self.fwd_in_splits)
         D, B = self.D, self.B
         for j in range(self.world):
             c = self.part.counts[j]
@@ -134,8 +144,8 @@ class ShardedHotPath:
             t0, _ = self.part.range(j)
             self.gsend[self.offsets[j]: self.offsets[j] + B * c * D].view(B, c * D).copy_(
                 self.dt[:, D + t0 * D: D + (t0 + c) * D])
-        dist.all_to_all_single(self.grecv.reshape(-1)[: self.Bg * self.Tr * self.D], self.gsend, self.bwd_out_splits,
-                               self.bwd_in_splits, group=self.group)
+        self._a2a(self.grecv.reshape(-1)[: self.Bg * self.Tr * self.D], self.gsend, self.bwd_out_splits,
+                  self.bwd_in_splits)
 
     # ---- the step
     def forward(self, x, idx):

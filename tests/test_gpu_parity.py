@@ -418,3 +418,72 @@ def test_host_tensors_are_rejected_before_launch(pkg, gpu):
     hp = pkg.HotPath(pkg.EmbeddingTableSet([torch.zeros((5, 16), device=gpu)]), 4, 1, index_base=0)
     with pytest.raises(ValueError):
         hp.validate(x, pkg.PackedIndices(torch.zeros((1, 4), dtype=torch.int32)))
+
+
+# ------------------------------------------------------------------ sharded (2 ranks on one GPU)
+def _gpu_shard_worker(rank, world, port, outdir):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
+    dev = torch.device("cuda:0")
+    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 64, 2
+    T, Bg = len(rows), B * world
+    rng = np.random.default_rng(7)
+    tabs = rand_tables(rng, rows, D)
+    idx = rand_indices(rng, rows, Bg, L)
+    x = rng.standard_normal((Bg, D)).astype(np.float32)
+    F = T + 1
+    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
+    part = TablePartition(T, world)
+    t0, t1 = part.range(rank)
+    ops = HipShardOps([torch.from_numpy(t).to(dev) for t in tabs[t0:t1]], Bg, L, 0.25)
+    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, dev)
+    p = pkg.PackedIndices(torch.from_numpy(idx[t0:t1]).to(torch.int32).reshape(t1 - t0, Bg, L).to(dev))
+    sl = slice(rank * B, (rank + 1) * B)
+    eng.step(torch.from_numpy(x[sl]).to(dev), p, torch.from_numpy(dout[sl]).to(dev))
+    torch.cuda.synchronize()
+    ops.ctx.check_bounds()
+    np.savez(os.path.join(outdir, f"g{rank}.npz"), out=eng.out.cpu().numpy(), dx=eng.dx.cpu().numpy(),
+             **{f"t{t}": ops.ts[t - t0].data.cpu().numpy() for t in range(t0, t1)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path):
+    """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange) equals the
+    single-GPU HotPath on the global batch bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method="spawn")
+    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 64, 2
+    T, Bg = len(rows), B * world
+    rng = np.random.default_rng(7)
+    tabs = rand_tables(rng, rows, D)
+    idx = rand_indices(rng, rows, Bg, L)
+    x = rng.standard_normal((Bg, D)).astype(np.float32)
+    F = T + 1
+    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), Bg, L, lr=0.25, index_base=0)
+    p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(T, Bg, L).to(gpu))
+    hp.step(torch.from_numpy(x).to(gpu), p, torch.from_numpy(dout).to(gpu))
+    from dlrm_jl_amd.sharded import TablePartition
+    part = TablePartition(T, world)
+    for r in range(world):
+        z = np.load(tmp_path / f"g{r}.npz")
+        sl = slice(r * B, (r + 1) * B)
+        assert np.array_equal(z["out"], to_np_f32(hp.out)[sl])
+        assert np.array_equal(z["dx"], to_np_f32(hp.dx)[sl])
+        for t in range(*part.range(r)):
+            assert np.array_equal(z[f"t{t}"], to_np_f32(hp.ts[t].data)), (r, t)
