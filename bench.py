@@ -42,20 +42,27 @@ def parse():
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
     ap.add_argument("--overlap-indexer", type=int, default=0)
     ap.add_argument("--fused", type=int, default=1)
+    ap.add_argument("--materialize-ys", type=int, default=-1,
+                    help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
+                         "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
+    ap.add_argument("--stage-timing", type=int, default=1, help="0: skip the per-stage telemetry (traces)")
     return ap.parse_args()
 
 
-def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks):
+def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks, materialize_ys=True):
     """Per-launch algorithmic HBM bytes of each stage (SURVEY.md §8d formulas)."""
     d, F = D, T + 1
     P = F * (F - 1) // 2
     N = B * L
+    ys_w = F * D * E if materialize_ys else 0  # the lookup output, when the forward writes it
+    # backward's T: the materialized ys, or x + the T gathered rows (and their indices)
+    t_r = F * D * E if materialize_ys else d * E + T * (I + D * E)
     return {
-        # fused maplookup + interaction: x, L rows + L indices per table in; ys (x + T rows) and out written
-        "lookup_interact_fwd": B * (d * E + T * L * (I + D * E) + F * D * E + (d + P) * E),
+        # fused maplookup + interaction: x, L rows + L indices per table in; (ys and) out written
+        "lookup_interact_fwd": B * (d * E + T * L * (I + D * E) + ys_w + (d + P) * E),
         "lookup": T * B * (L * I + L * D * E + D * E),
         "interact_fwd": B * (d * E + (F - 1) * D * E + d * E + (d + P) * E),
-        "interact_bwd": B * ((d + P) * E + F * D * E + F * D * 4 + d * 4),
+        "interact_bwd": B * ((d + P) * E + t_r + F * D * 4 + d * 4),
         "indexer_build": T * N * I + T * N * 4 + uniq * 8 + chunks * 16,
         "sgd_update": T * N * (4 + D * 4) + uniq * 2 * D * E + chunks * 16,
     }
@@ -160,7 +167,8 @@ def main():
         tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows)
         ts = pkg.EmbeddingTableSet(tables)
         engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0, overlap_indexer=bool(a.overlap_indexer),
-                             fused=bool(a.fused))
+                             fused=bool(a.fused),
+                             materialize_ys=None if a.materialize_ys < 0 else bool(a.materialize_ys))
         F = T + 1
         dtp = tables[0].dtype
         x = torch.randn((B, D), device=dev, generator=g).to(dtp)
@@ -186,7 +194,11 @@ def main():
     elif engine.ops is not None:
         engine.ops.ctx.check_bounds()
 
+    # hipGraphs: one graph holds NBATCH consecutive steps (one per index batch), so the
+    # per-replay launch gap (~8 us measured on MI355X) is paid once per NBATCH steps; single-step
+    # graphs cover a remainder.  Within a graph the kernels run back to back.
     graphs = None
+    multi = None
     if a.mode == "graph":
         try:
             graphs = []
@@ -198,26 +210,35 @@ def main():
                     with torch.cuda.graph(gr, stream=s):
                         step(k)
                     graphs.append(gr)
+                multi = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(multi, stream=s):
+                    for k in range(NBATCH):
+                        step(k)
             torch.cuda.current_stream().wait_stream(s)
             for k in range(NBATCH):
                 graphs[k].replay()
+            multi.replay()
             torch.cuda.synchronize()
         except Exception as e:  # graph capture unsupported: eager
             print(f"note: graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
-            graphs = None
+            graphs = multi = None
 
-    def run(k):
-        if graphs is not None:
-            graphs[k % NBATCH].replay()
-        else:
-            step(k)
+    def run_steps(n):
+        """n consecutive steps starting at batch 0."""
+        if graphs is None:
+            for k in range(n):
+                step(k)
+            return
+        for _ in range(n // NBATCH):
+            multi.replay()
+        for k in range(n % NBATCH):
+            graphs[k].replay()
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        run(k)
+    run_steps(a.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -232,7 +253,7 @@ def main():
     # ---- per-kernel timing (HIP events on the launch stream) + roofline, rank 0
     roofline = None
     stages = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and a.stage_timing:
         uniq = chunks = 0
         for k in range(NBATCH):
             engine.build_indexer(packs[k])
@@ -241,7 +262,7 @@ def main():
                 uniq += len(engine.indexer.unique_rows(t))
         uniq /= NBATCH
         chunks = uniq  # one chunk per unique row, plus a few for hot rows
-        bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks)
+        bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks, engine.materialize_ys)
         # one prebuilt indexer per index batch, so the update stage can be timed on its own
         indexers = [pkg.SparseIndexer(T, B * L, dev) for _ in range(NBATCH)]  # not the engine's own
         home = engine.indexer
@@ -258,11 +279,12 @@ def main():
         if engine.fused:
             names = ["lookup_interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: engine.build_indexer(packs[k]),
-                   lambda k: engine.interact_bwd(dout), apply_k]
+                   lambda k: engine.interact_bwd(dout, x=x, idx=packs[k]), apply_k]
         else:
             names = ["lookup", "interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
             fns = [lambda k: engine.lookup(packs[k]), lambda k: engine.interact_fwd(x),
-                   lambda k: engine.build_indexer(packs[k]), lambda k: engine.interact_bwd(dout), apply_k]
+                   lambda k: engine.build_indexer(packs[k]), lambda k: engine.interact_bwd(dout, x=x, idx=packs[k]),
+                   apply_k]
         # Each stage: a hipGraph of its kernel(s) over the NBATCH index batches (the same batches the
         # timed loop cycles, so caches are no warmer than there), replayed REPS times between two HIP
         # events on the launch stream; per-launch time = elapsed / (REPS * NBATCH).  Back-to-back
@@ -323,7 +345,9 @@ def main():
             "config": {"workload": a.workload, "tables": T, "dim": D, "batch_per_gpu": B, "global_batch": B * world,
                        "lookups": L, "index_dtype": "int32", "table_rows": "Criteo-Kaggle (criteo.jl:350-377)",
                        "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + RCCL all-to-all",
-                       "launch": "hipGraph replay" if graphs is not None else "eager"},
+                       "launch": f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else "eager",
+                       "ys": ("materialized" if world > 1 or engine.materialize_ys
+                              else "not materialized (backward re-gathers T)")},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -36,6 +36,7 @@ struct dlrm_indexer {
     int T = 0;
     IndexerDev dev{};
     void* block = nullptr;  // one allocation for every array
+    void* partial_big = nullptr;  // partial rows for D > kPartialDim (allocated on first use)
     // recorded by the last build
     bool built = false;
     const void* indices = nullptr;
@@ -248,12 +249,16 @@ int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, const void* i
     if (rc) return rc;
     const int d = tb->D, F = tb->T + 1;
     const int64_t P = (int64_t)F * (F - 1) / 2;
-    CHECK_ARG(padding >= 0 && x_ld >= d && ys_ld >= (int64_t)F * d && out_ld >= d + P + padding,
+    CHECK_ARG(padding >= 0 && x_ld >= d && (!ys || ys_ld >= (int64_t)F * d) && out_ld >= d + P + padding,
               "dlrm_lookup_interact_fwd: leading dimensions too small");
-    CHECK_ARG(batch == 0 || (x && ys && out), "dlrm_lookup_interact_fwd: null buffer");
+    CHECK_ARG(batch == 0 || (x && out), "dlrm_lookup_interact_fwd: null buffer");
     rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                     index_base, lookups, d, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
     if (rc != DLRM_E_UNSUPPORTED) return rc;
+    if (!ys)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
+                        "dlrm_lookup_interact_fwd: ys may be NULL only where the fused kernel applies "
+                        "(16-B aligned rows, F <= 96)");
     rc = launch_maplookup(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype, table_stride,
                           index_base, batch, lookups, ys, ys_ld, d);
     if (rc) return rc;
@@ -274,6 +279,24 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
     return launch_interact_bwd(ctx, dtype, d, num_features, batch, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
 }
 
+int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
+                             int64_t table_stride, int index_base, int batch, int lookups, const void* x,
+                             int64_t x_ld, const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld,
+                             float* dt, int64_t dt_ld) {
+    CHECK_ARG(ctx && tb, "dlrm_interact_bwd_gather: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    CHECK_ARG(lookups == 1, "dlrm_interact_bwd_gather: one-hot lookups only (L=%d: use dlrm_interact_bwd on ys)",
+              lookups);
+    const int d = tb->D, F = tb->T + 1;
+    const int64_t P = (int64_t)F * (F - 1) / 2;
+    CHECK_ARG(padding >= 0 && x_ld >= d && dout_ld >= d + P + padding && dx_ld >= d && dt_ld >= (int64_t)F * d,
+              "dlrm_interact_bwd_gather: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (x && dout && dx && dt), "dlrm_interact_bwd_gather: null buffer");
+    return launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                      index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld);
+}
+
 // --------------------------------------------------------------------------- indexer
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm_indexer** out) {
     CHECK_ARG(ctx && out, "dlrm_indexer_create: null argument");
@@ -287,6 +310,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
     const int64_t T = num_tables > 0 ? num_tables : 1;
     ix->dev.cap = cap;
+    ix->dev.pcap = indexer_slice_cap(cap);
+    ix->dev.pdim = kPartialDim;
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
     const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1));
@@ -294,6 +319,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.keys0, n * 4},     {(void**)&ix->dev.keys1, n * 4},   {(void**)&ix->dev.vals0, n * 4},
         {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
         {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot, n * 16},
+        {(void**)&ix->dev.hot_slice, n * 4}, {(void**)&ix->dev.hot_cnt, n * 4},
+        {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},
     };
     size_t total = 0;
@@ -318,6 +345,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
 int dlrm_indexer_destroy(dlrm_indexer* ix) {
     if (!ix) return DLRM_OK;
     if (ix->block) (void)hipFree(ix->block);
+    if (ix->partial_big) (void)hipFree(ix->partial_big);
     delete ix;
     return DLRM_OK;
 }
@@ -399,6 +427,18 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned f
     } else {
         rc = dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, lookups);
         if (rc) return rc;
+    }
+    if (tb->D > ix->dev.pdim) {  // multi-slice hot segments keep partial rows of D elements
+        void* p = nullptr;
+        rc = hip_set(ctx);
+        if (rc == DLRM_OK)
+            rc = ctx_hip(ctx, hipMalloc(&p, (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.pcap * tb->D * 4),
+                         "hipMalloc(indexer partials)");
+        if (rc) return rc;
+        if (ix->partial_big) (void)hipFree(ix->partial_big);
+        ix->partial_big = p;
+        ix->dev.partial = (float*)p;
+        ix->dev.pdim = tb->D;
     }
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
                             (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr);

@@ -86,10 +86,17 @@ struct IndexerDev {
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
     int4* chunks;          // segments of <= kChunk positions: {beg, end, row, first position}
-    int4* hot;             // longer segments: {beg, end, row, 0}, one workgroup each
-    int32_t* counts;       // [T][8]: U, chunks, hot, -, nvalid
+    int4* hot;             // longer segments: {beg, end, row, first slice}
+    int32_t* hot_slice;    // slice -> its hot segment (slices of kHotSlice positions)
+    int32_t* hot_cnt;      // arrivals per hot segment (multi-slice combine; reset by the last)
+    float* partial;        // [T][pcap][pdim] slice partial sums (multi-slice hot segments)
+    int32_t* counts;       // [T][8]: U, chunks, hot, slices, nvalid
     int64_t cap;
+    int64_t pcap;          // slices per table (upper bound)
+    int pdim;              // partial row capacity (elements)
 };
+int64_t indexer_slice_cap(int64_t cap);
+constexpr int kPartialDim = 256;  // partial rows allocated with the indexer (larger D: regrown on use)
 
 }  // namespace dlrm
 
@@ -111,6 +118,10 @@ int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld,
                                int padding);
+int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
+                               const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                               const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
+                               int64_t dx_ld, float* dt, int64_t dt_ld);
 int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,

@@ -94,28 +94,29 @@ struct GatherArgs {
     unsigned* err;
 };
 
-template <typename T, int NB, bool FUSED>
-__global__ __launch_bounds__(256) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x, int64_t x_ld,
-                                                           T* __restrict__ ys, int64_t ys_ld, T* __restrict__ out,
-                                                           int64_t out_ld, int padding, GatherArgs ga) {
+template <typename T, int NB, bool FUSED, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
+                                                                int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
+                                                                T* __restrict__ out, int64_t out_ld, int padding,
+                                                                GatherArgs ga) {
     typedef Frag<T> FR;
     typedef typename FR::type frag;
     constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
-    __shared__ float stage_all[4][kStage];
+    __shared__ float stage_all[WPB][kStage];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
     const int P = F * (F - 1) / 2;
     const int W = d + P + padding;
     const bool staged = W <= kStage;
     float* stage = stage_all[w];
-    for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < B; b += (int64_t)gridDim.x * 4) {
+    for (int64_t b = (int64_t)blockIdx.x * WPB + w; b < B; b += (int64_t)gridDim.x * WPB) {
         const T* xb = x + b * x_ld;
-        T* yb = ys + b * ys_ld;
+        T* yb = ys ? ys + b * ys_ld : nullptr;  // FUSED: ys may be NULL (not materialized)
         T* orow = out + b * out_ld;
         // fast_vcat: x into the reserved rows of ys; x is also the head of the output row.
         for (int i = lane; i < d; i += 64) {
             const T v = xb[i];
-            yb[i] = v;
+            if (yb) yb[i] = v;
             if (staged) stage[i] = to_f32(v);
             else orow[i] = v;
         }
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(256) void interact_fwd_kernel(int d, int F, int B, 
                     }
                 }
                 // the lookup output: ys rows 1..F-1 written from the fragments
+                if (yb)
 #pragma unroll
                 for (int uu = 0; uu < UU; ++uu) {
                     const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
@@ -250,11 +252,14 @@ __device__ __forceinline__ f32x4_t load4_f32(const uint16_t* p) {
 // operand of the MFMA that produces output columns 64sb + 4j + e.  The four accumulators of
 // a tile row then hold 4 consecutive output columns per lane -> one float4 store per row.
 // All k-step loads of a super-block are issued before its MFMAs (up to 4*NB in flight).
-template <typename T, int NB>
+// GATHER: T_b is not read from a materialized ys but rebuilt from x (row 0) and the table
+// rows of the sample's one-hot indices (rows 1..F-1): the same values, without ys.
+template <typename T, int NB, bool GATHER>
 __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
                                                            int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
                                                            float* __restrict__ dx, int64_t dx_ld,
-                                                           float* __restrict__ dt, int64_t dt_ld) {
+                                                           float* __restrict__ dt, int64_t dt_ld, GatherArgs ga,
+                                                           const T* __restrict__ x, int64_t x_ld) {
     typedef BwdGeom<NB> G;
     constexpr int KS = 4 * NB;  // max k-steps (F <= 16 NB)
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -266,7 +271,24 @@ __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, 
     const int ksteps = (F + 3) / 4;
     for (int64_t b = (int64_t)blockIdx.x * G::WPB + w; b < B; b += (int64_t)gridDim.x * G::WPB) {
         const T* ob = dout + b * dout_ld;
-        const T* tb = t + b * t_ld;
+        const T* tb = GATHER ? nullptr : t + b * t_ld;
+        const T* rowp[KS];  // GATHER: this lane's T rows kk = 4s + q
+        if (GATHER) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int kk = 4 * s + q;
+                rowp[s] = nullptr;
+                if (s < ksteps && kk < F) {
+                    if (kk == 0) {
+                        rowp[s] = x + b * x_ld;
+                    } else {
+                        const int64_t r = load_index(ga.idx, ga.itype, (kk - 1) * ga.tstride + b * ga.L) - ga.base;
+                        if (r >= 0 && r < ga.tabs[kk - 1].nrows) rowp[s] = (const T*)ga.tabs[kk - 1].data + r * d;
+                        else if (c == 0) raise_index_error(ga.err);
+                    }
+                }
+            }
+        }
         // S: zero, then scatter the packed pairs to both triangles (fused unpack + transpose-add)
         for (int e = lane; e < G::NS * G::NS; e += 64) S[(e / G::NS) * G::SS + (e % G::NS)] = 0.0f;
         wave_lds_sync();
@@ -287,8 +309,8 @@ __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, 
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const int kk = 4 * s + q;
-                bv[s] = (s < ksteps && kk < F && colok) ? load4_f32(tb + (int64_t)kk * d + n0)
-                                                        : f32x4_t{0.f, 0.f, 0.f, 0.f};
+                const T* src = GATHER ? rowp[s] : (kk < F ? tb + (int64_t)kk * d : nullptr);
+                bv[s] = (s < ksteps && src && colok) ? load4_f32(src + n0) : f32x4_t{0.f, 0.f, 0.f, 0.f};
             }
             f32x4_t acc[NB][4];
 #pragma unroll
@@ -361,11 +383,25 @@ __global__ __launch_bounds__(256) void interact_fwd_scalar(int d, int F, int B, 
     }
 }
 
-template <typename T>
+template <typename T, bool GATHER>
+__device__ __forceinline__ float t_elem(const T* t, int64_t t_ld, int64_t b, int j, int n, int d, const GatherArgs& ga,
+                                        const T* x, int64_t x_ld) {
+    if (!GATHER) return to_f32(t[b * t_ld + (int64_t)j * d + n]);
+    if (j == 0) return to_f32(x[b * x_ld + n]);
+    const int64_t r = load_index(ga.idx, ga.itype, (j - 1) * ga.tstride + b * ga.L) - ga.base;
+    if (r < 0 || r >= ga.tabs[j - 1].nrows) {
+        raise_index_error(ga.err);
+        return 0.0f;
+    }
+    return to_f32(((const T*)ga.tabs[j - 1].data)[r * d + n]);
+}
+
+template <typename T, bool GATHER>
 __global__ __launch_bounds__(256) void interact_bwd_scalar(int d, int F, int B, const T* __restrict__ dout,
                                                            int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
                                                            float* __restrict__ dx, int64_t dx_ld,
-                                                           float* __restrict__ dt, int64_t dt_ld) {
+                                                           float* __restrict__ dt, int64_t dt_ld, GatherArgs ga,
+                                                           const T* __restrict__ x, int64_t x_ld) {
     const int64_t total = (int64_t)B * F * d;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t b = e / ((int64_t)F * d);
@@ -376,7 +412,7 @@ __global__ __launch_bounds__(256) void interact_bwd_scalar(int d, int F, int B, 
         for (int j = 0; j < F; ++j) {
             if (j == f) continue;
             const int hi = j > f ? j : f, lo = j > f ? f : j;
-            acc = fmaf(to_f32(t[b * t_ld + (int64_t)j * d + n]), to_f32(ob[hi * (hi - 1) / 2 + lo]), acc);
+            acc = fmaf(t_elem<T, GATHER>(t, t_ld, b, j, n, d, ga, x, x_ld), to_f32(ob[hi * (hi - 1) / 2 + lo]), acc);
         }
         dt[b * dt_ld + (int64_t)f * d + n] = acc;
         if (f == 0) dx[b * dx_ld + n] = to_f32(dout[b * dout_ld + n]) + acc;
@@ -409,16 +445,6 @@ static bool dispatch_fwd(int NB, hipStream_t s, int cus, int d, int F, int B, co
 #undef DLRM_CASE
         default: return false;
     }
-}
-
-template <typename T, int NB>
-static void launch_bwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* dout, int64_t dout_ld,
-                          const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
-    typedef BwdGeom<NB> G;
-    const unsigned g = grid_for(B, G::WPB, cus);
-    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB;
-    hipLaunchKernelGGL((interact_bwd_kernel<T, NB>), dim3(g), dim3(64 * G::WPB), lds, s, d, F, B, (const T*)dout,
-                       dout_ld, (const T*)t, t_ld, dx, dx_ld, dt, dt_ld);
 }
 
 static bool fwd_aligned(int dtype, int d, const void* x, int64_t x_ld, const void* ys, int64_t ys_ld) {
@@ -473,42 +499,78 @@ int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
     return ctx_hip(ctx, hipGetLastError(), "lookup_interact_fwd launch");
 }
 
-template <typename T>
+template <typename T, int NB, bool GATHER>
+static void launch_bwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* dout, int64_t dout_ld,
+                          const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld,
+                          const GatherArgs& ga, const void* x, int64_t x_ld) {
+    typedef BwdGeom<NB> G;
+    const unsigned g = grid_for(B, G::WPB, cus);
+    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB;
+    hipLaunchKernelGGL((interact_bwd_kernel<T, NB, GATHER>), dim3(g), dim3(64 * G::WPB), lds, s, d, F, B,
+                       (const T*)dout, dout_ld, (const T*)t, t_ld, dx, dx_ld, dt, dt_ld, ga, (const T*)x, x_ld);
+}
+
+template <typename T, bool GATHER>
 static void dispatch_bwd(int NB, hipStream_t s, int cus, int d, int F, int B, const void* dout, int64_t dout_ld,
-                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
+                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld,
+                         const GatherArgs& ga, const void* x, int64_t x_ld) {
     switch (NB) {
-        case 1: launch_bwd_nb<T, 1>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 2: launch_bwd_nb<T, 2>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 3: launch_bwd_nb<T, 3>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 4: launch_bwd_nb<T, 4>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 5: launch_bwd_nb<T, 5>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 6: launch_bwd_nb<T, 6>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
-        case 7: launch_bwd_nb<T, 7>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld); break;
+#define DLRM_CASE(N)                                                                                               \
+    case N:                                                                                                        \
+        launch_bwd_nb<T, N, GATHER>(s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, ga, x, x_ld); \
+        break;
+        DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(3) DLRM_CASE(4) DLRM_CASE(5) DLRM_CASE(6) DLRM_CASE(7)
+#undef DLRM_CASE
     }
 }
 
-int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
-                        const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
+// dT = S T per sample; T from `t` (materialized ys) or, GATHER, from x + the table rows.
+template <bool GATHER>
+static int run_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
+                            const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld,
+                            const GatherArgs& ga, bool rows_aligned, const void* x, int64_t x_ld) {
     if (B == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     const int NB = (F + 15) / 16;
     const int esz = dtype == DLRM_F32 ? 4 : 2;
-    const bool aligned = d % 4 == 0 && (uintptr_t)t % (4 * esz) == 0 && (t_ld % 4) == 0 && (uintptr_t)dx % 16 == 0 &&
-                         (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 && (dt_ld % 4) == 0;
+    const bool t_ok = GATHER ? (rows_aligned && (uintptr_t)x % (4 * esz) == 0 && (x_ld % 4) == 0)
+                             : ((uintptr_t)t % (4 * esz) == 0 && (t_ld % 4) == 0);
+    const bool aligned = d % 4 == 0 && t_ok && (uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 &&
+                         (dt_ld % 4) == 0;
     if (aligned && NB >= 1 && NB <= 7) {  // NB = 8 would need > 64 KB of dynamic LDS
-        if (dtype == DLRM_F32) dispatch_bwd<float>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
-        else dispatch_bwd<uint16_t>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
+        if (dtype == DLRM_F32)
+            dispatch_bwd<float, GATHER>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, ga, x, x_ld);
+        else
+            dispatch_bwd<uint16_t, GATHER>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, ga, x,
+                                           x_ld);
     } else {
         const unsigned g = grid_for((int64_t)B * F * d, 256, cus);
         if (dtype == DLRM_F32)
-            hipLaunchKernelGGL(interact_bwd_scalar<float>, dim3(g), dim3(256), 0, s, d, F, B, (const float*)dout,
-                               dout_ld, (const float*)t, t_ld, dx, dx_ld, dt, dt_ld);
+            hipLaunchKernelGGL((interact_bwd_scalar<float, GATHER>), dim3(g), dim3(256), 0, s, d, F, B,
+                               (const float*)dout, dout_ld, (const float*)t, t_ld, dx, dx_ld, dt, dt_ld, ga,
+                               (const float*)x, x_ld);
         else
-            hipLaunchKernelGGL(interact_bwd_scalar<uint16_t>, dim3(g), dim3(256), 0, s, d, F, B,
-                               (const uint16_t*)dout, dout_ld, (const uint16_t*)t, t_ld, dx, dx_ld, dt, dt_ld);
+            hipLaunchKernelGGL((interact_bwd_scalar<uint16_t, GATHER>), dim3(g), dim3(256), 0, s, d, F, B,
+                               (const uint16_t*)dout, dout_ld, (const uint16_t*)t, t_ld, dx, dx_ld, dt, dt_ld, ga,
+                               (const uint16_t*)x, x_ld);
     }
     return ctx_hip(ctx, hipGetLastError(), "interact_bwd launch");
+}
+
+int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
+                        const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld) {
+    return run_interact_bwd<false>(ctx, dtype, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, GatherArgs{},
+                                   true, nullptr, 0);
+}
+
+int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
+                               const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                               const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
+                               int64_t dx_ld, float* dt, int64_t dt_ld) {
+    GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
+    return run_interact_bwd<true>(ctx, dtype, d, T_ + 1, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt, dt_ld, ga,
+                                  tabs_aligned16, x, x_ld);
 }
 
 }  // namespace dlrm

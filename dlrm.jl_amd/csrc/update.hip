@@ -33,9 +33,42 @@ constexpr int kChunk = 32;          // max positions of a segment handled by one
 constexpr int kLdsSortMax = 2048;   // positions per table sorted entirely in LDS
 constexpr int kDigits = 257;        // 256 row digits + 1 bucket that keeps invalid indices last
 constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
-constexpr int kHotChunksMax = 16;   // LDS partials per hot segment
 
-enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_NV = 4 };
+enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
+
+// Hot segments are cut into slices of kHotSlice positions, one work item each; a segment of
+// several slices is combined by its last-arriving slice (sc1 partial rows + a counter).
+constexpr int kHotSlice = 128;
+int64_t indexer_slice_cap(int64_t cap) { return cap / kHotSlice + cap / (kChunk + 1) + 1; }
+
+#ifdef DLRM_PHASE
+// Phase timestamps (wall_clock64, 100 MHz) of one indexer block + start/end of every block;
+// built only into the profiling variant of the library (tools/phase_indexer.py).
+__device__ unsigned long long g_phase[64];
+__device__ unsigned long long g_blk[2][256];
+#define PHASE(k) do { __syncthreads(); if (blockIdx.x == DLRM_PHASE && threadIdx.x == 0) g_phase[k] = wall_clock64(); } while (0)
+__device__ unsigned long long g_apply[3][32768];  // start, end, kind of every apply block
+#define APPLY_START(kind) do { if (threadIdx.x == 0) { const int blk_ = blockIdx.y * gridDim.x + blockIdx.x; \
+    if (blk_ < 32768) { g_apply[0][blk_] = wall_clock64(); g_apply[2][blk_] = (kind); } } } while (0)
+#define APPLY_END() do { if ((threadIdx.x & 63) == 0) { const int blk_ = blockIdx.y * gridDim.x + blockIdx.x; \
+    if (blk_ < 32768) atomicMax(&g_apply[1][blk_], wall_clock64()); } } while (0)
+extern "C" int dlrm_debug_phase(unsigned long long* out) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase));
+    return (int)hipMemcpyFromSymbol(out + 64, HIP_SYMBOL(g_blk), sizeof(g_blk));
+}
+extern "C" int dlrm_debug_apply(unsigned long long* out) {
+    hipMemset(g_apply, 0, 0);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_apply), sizeof(g_apply));
+}
+extern "C" int dlrm_debug_apply_reset(void) {
+    static unsigned long long z[3][32768];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_apply), z, sizeof(z));
+}
+#else
+#define PHASE(k) do {} while (0)
+#define APPLY_START(kind) do {} while (0)
+#define APPLY_END() do {} while (0)
+#endif
 
 // Exclusive scan over the 1024 threads of the block; returns this thread's prefix, total in *tot.
 template <typename V>
@@ -94,6 +127,7 @@ __device__ void radix_pass(int N, int shift, bool first_pass, uint32_t sentinel,
         const int v = tid < kDigits ? sl.hist[tid] : 0;
         int tot;
         const int ex = block_scan_excl<int>(v, sl.wtot, &tot);
+        PHASE(first_pass ? 3 : 13);
         if (tid < kDigits) {
             sl.digit_off[tid] = ex;
             if (first_pass) sl.bucket_start[tid] = ex;
@@ -112,6 +146,7 @@ __device__ void radix_pass(int N, int shift, bool first_pass, uint32_t sentinel,
         }
         __syncthreads();
     }
+    PHASE(first_pass ? 4 : 14);
     for (int tile = 0; tile < N; tile += kBuildThreads) {
         const int i = tile + tid;
         const bool valid = i < N;
@@ -145,6 +180,7 @@ __device__ void radix_pass(int N, int shift, bool first_pass, uint32_t sentinel,
             vout[dst] = val;
         }
         __syncthreads();
+        PHASE(first_pass ? 5 + tile / kBuildThreads : 15);
     }
 }
 
@@ -181,11 +217,13 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
         U += tot;
     }
     __syncthreads();
+    PHASE(20);
     const int nvalid = sl.nvalid;
     if (tid == 0) seg_start[U] = nvalid;
     int4* chunks = ix.chunks + off;
     int4* hot = ix.hot + off;
-    long long C = 0, H = 0;
+    int32_t* hot_slice = ix.hot_slice + off;
+    long long C = 0, H = 0, S = 0;
     for (int tile = 0; tile < U; tile += kBuildThreads) {
         const int s = tile + tid;
         int beg = 0, end = 0;
@@ -195,16 +233,25 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
         }
         const bool isc = s < U && end - beg <= kChunk;
         const bool ish = s < U && end - beg > kChunk;
-        long long tot;
+        const int ns = ish ? (end - beg + kHotSlice - 1) / kHotSlice : 0;
+        long long tot, tots;
         const long long ex = block_scan_excl<long long>((isc ? 1ll : 0ll) | ((ish ? 1ll : 0ll) << 32), sl.wtot64, &tot);
+        const long long exs = block_scan_excl<long long>((long long)ns, sl.wtot64, &tots);
         if (isc) chunks[C + (ex & 0xffffffffll)] = make_int4(beg, end, (int)srow[s], V[beg]);
-        if (ish) hot[H + (ex >> 32)] = make_int4(beg, end, (int)srow[s], 0);
+        if (ish) {
+            const int h = (int)(H + (ex >> 32));
+            const int s0 = (int)(S + exs);
+            hot[h] = make_int4(beg, end, (int)srow[s], s0);
+            for (int k = 0; k < ns; ++k) hot_slice[s0 + k] = h;
+        }
         C += tot & 0xffffffffll;
         H += tot >> 32;
+        S += tots;
     }
+    PHASE(21);
     if (tid == 0) {
         int32_t* cnt = ix.counts + (int64_t)t * 8;
-        cnt[CNT_U] = U; cnt[CNT_C] = (int)C; cnt[CNT_H] = (int)H; cnt[CNT_NV] = nvalid;
+        cnt[CNT_U] = U; cnt[CNT_C] = (int)C; cnt[CNT_H] = (int)H; cnt[CNT_S] = (int)S; cnt[CNT_NV] = nvalid;
     }
 }
 
@@ -214,6 +261,10 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
     int64_t tstride, int base, int B, int L, unsigned* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     __shared__ SortLds sl;
+#ifdef DLRM_PHASE
+    if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
+#endif
+    PHASE(0);
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
     const int N = B * L;
@@ -242,6 +293,7 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
         vbuf[0][i] = i;
     }
     __syncthreads();
+    PHASE(1);
     radix_pass(N, 0, true, sentinel, kbuf[0], vbuf[0], kbuf[1], vbuf[1], sl);
     int cur = 1;
     if (nbits > 8) {
@@ -266,6 +318,7 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
                 vbuf[0][bs + rank] = vbuf[1][i];
             }
             __syncthreads();
+            PHASE(10);
             cur = 0;
         } else {
             // skewed rows: the remaining LSD passes (the sentinel keeps digit 256: stays last)
@@ -276,6 +329,285 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
         }
     }
     build_segments(ix, t, kbuf[cur], vbuf[cur], N, sentinel, vbuf[cur ^ 1], kbuf[cur ^ 1], sl);
+    PHASE(22);
+#ifdef DLRM_PHASE
+    if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
+#endif
+}
+
+// ------------------------------------------------------------------- fast indexer (N <= 4096)
+// One 1024-thread workgroup per table; everything stays in LDS.
+//  * Stable counting pass on an 8-bit digit: wave w walks positions [w*S, (w+1)*S) (S = 64*EPL)
+//    in tiles of 64, so "earlier position" = earlier wave, earlier tile or lower lane.  Lanes
+//    sharing a digit are found with 8 ballots; each wave keeps its running count of every
+//    digit in its own column of cnt[digit][wave] (only that wave touches it, in program
+//    order), which gives each key its rank among the wave's earlier equal digits.  One block
+//    scan over cnt in (digit, wave) order turns the counts into output offsets: no serial
+//    cross-wave loop.  Invalid indices are dropped (they raised the bounds flag).
+//  * Rows of <= 8 bits are then grouped.  Larger rows: when every bucket is small (uniform
+//    rows: N/256 keys per bucket) each bucket is ordered by a direct rank on (row, position);
+//    skewed rows take the remaining LSD passes.
+//  * Segments and the chunk / hot lists: one head-flag scan and one packed 64-bit scan.
+// Output format = indexer_build_kernel's (the apply kernel and dlrm_indexer_read unchanged).
+constexpr int kFastThreads = 1024;
+constexpr int kFastWaves = kFastThreads / 64;
+constexpr int kFastBits = 8;
+constexpr int kFastDigits = 1 << kFastBits;
+constexpr int kFastMaxN = 4096;
+static_assert(kFastDigits * kFastWaves == 4 * kFastThreads, "4 (digit, wave) counters per thread");
+
+template <int EPL>
+struct FastLds {
+    uint16_t cnt[kFastDigits][kFastWaves];  // digit-major: per-wave counts, then output offsets
+    uint16_t bstart[kFastDigits + 8];       // first-pass bucket starts
+    uint32_t K[2][kFastThreads * EPL];
+    int32_t V[2][kFastThreads * EPL];
+    int wtot[2 * kFastWaves];
+    long long wtot64[2 * kFastWaves];
+    int maxbucket;
+};
+
+// One stable counting pass.  FROM_REGS: the first pass's keys come from registers (tile j
+// of wave w = position w*S + 64j + lane); otherwise from kin/vin[0, n) in LDS.  Returns the
+// number of keys written to kout/vout.
+template <int EPL, bool FROM_REGS>
+__device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bool (&rok)[EPL],
+                         const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                         FastLds<EPL>& sl, bool first) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    constexpr int S = 64 * EPL;
+    ((uint2*)&sl.cnt[0][0])[tid] = make_uint2(0, 0);  // 4 counters per thread
+    uint32_t key[EPL];
+    int32_t val[EPL];
+    bool ok[EPL];
+    int lr[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        if (FROM_REGS) {
+            key[j] = rkey[j];
+            ok[j] = rok[j];
+            val[j] = i;
+        } else {
+            ok[j] = i < n;
+            key[j] = ok[j] ? kin[i] : 0u;
+            val[j] = ok[j] ? vin[i] : 0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const uint32_t d = (key[j] >> shift) & (kFastDigits - 1);
+        unsigned long long peers = __ballot(ok[j]);
+#pragma unroll
+        for (int bit = 0; bit < kFastBits; ++bit) {
+            const unsigned long long bb = __ballot(ok[j] && ((d >> bit) & 1u));
+            peers &= ((d >> bit) & 1u) ? bb : ~bb;
+        }
+        int base = 0;
+        if (ok[j] && j > 0) base = sl.cnt[d][w];
+        lr[j] = base + __popcll(peers & lt);
+        if (ok[j] && (peers & lt) == 0) sl.cnt[d][w] = (uint16_t)(base + __popcll(peers));
+    }
+    __syncthreads();
+    // (digit, wave) offsets: thread tid owns counters [4 tid, 4 tid + 4) = digit tid/4, waves 4(tid%4)..
+    const uint2 raw = ((const uint2*)&sl.cnt[0][0])[tid];
+    const int c0 = raw.x & 0xffff, c1 = raw.x >> 16, c2 = raw.y & 0xffff, c3 = raw.y >> 16;
+    int total;
+    const int ex = block_scan_excl<int>(c0 + c1 + c2 + c3, sl.wtot, &total);
+    ((uint2*)&sl.cnt[0][0])[tid] =
+        make_uint2((uint32_t)ex | ((uint32_t)(ex + c0) << 16), (uint32_t)(ex + c0 + c1) | ((uint32_t)(ex + c0 + c1 + c2) << 16));
+    if (first) {
+        if ((tid & 3) == 0) sl.bstart[tid >> 2] = (uint16_t)ex;
+        if (tid == 0) {
+            sl.bstart[kFastDigits] = (uint16_t)total;
+            sl.maxbucket = 0;
+        }
+    }
+    __syncthreads();
+    if (first) {
+        // largest bucket (decides rank sort vs more passes): digit d's size = bstart[d+1] - bstart[d]
+        int m = tid < kFastDigits ? (int)sl.bstart[tid + 1] - (int)sl.bstart[tid] : 0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if (lane == 0 && m > 0) atomicMax(&sl.maxbucket, m);
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j)
+        if (ok[j]) {
+            const uint32_t d = (key[j] >> shift) & (kFastDigits - 1);
+            const int dst = sl.cnt[d][w] + lr[j];
+            kout[dst] = key[j];
+            vout[dst] = val[j];
+        }
+    __syncthreads();
+    return total;
+}
+
+template <int EPL>
+__device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, const void* __restrict__ idx,
+                                 int itype, int64_t tstride, int base, int N, unsigned* __restrict__ err,
+                                 FastLds<EPL>& sl) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int S = 64 * EPL;
+    const int nbits = 32 - __clz(nrows > 0 ? nrows - 1 : 0);
+    // the indices, read once (coalesced 64-lane runs, all loads in flight) and validated
+    uint32_t key[EPL];
+    bool ok[EPL];
+    int64_t raw[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        raw[j] = load_index(idx, itype, t * tstride + min(i, N - 1));
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        const int64_t r = raw[j] - base;
+        ok[j] = i < N && r >= 0 && r < (int64_t)nrows;
+        key[j] = ok[j] ? (uint32_t)r : 0u;
+        if (i < N && !ok[j]) raise_index_error(err);
+    }
+    PHASE(1);
+    const int n = fast_pass<EPL, true>(N, 0, key, ok, nullptr, nullptr, sl.K[1], sl.V[1], sl, true);
+    PHASE(5);
+    int cur = 1;
+    if (nbits > kFastBits) {
+        if (sl.maxbucket <= kRankBucketMax) {
+            // order each bucket by (row, position); the stable pass kept positions ascending
+#pragma unroll
+            for (int q = 0; q < EPL; ++q) {
+                const int i = tid + q * kFastThreads;
+                if (i >= n) continue;
+                const uint32_t ki = sl.K[1][i];
+                const int d = ki & (kFastDigits - 1);
+                const int bs = sl.bstart[d], be = sl.bstart[d + 1];
+                int rank = 0;
+                int j = bs;
+                for (; j + 4 <= be; j += 4) {
+                    const uint32_t k0 = sl.K[1][j], k1 = sl.K[1][j + 1], k2 = sl.K[1][j + 2], k3 = sl.K[1][j + 3];
+                    rank += (k0 < ki || (k0 == ki && j < i)) + (k1 < ki || (k1 == ki && j + 1 < i)) +
+                            (k2 < ki || (k2 == ki && j + 2 < i)) + (k3 < ki || (k3 == ki && j + 3 < i));
+                }
+                for (; j < be; ++j) {
+                    const uint32_t kj = sl.K[1][j];
+                    rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+                }
+                sl.K[0][bs + rank] = ki;
+                sl.V[0][bs + rank] = sl.V[1][i];
+            }
+            __syncthreads();
+            cur = 0;
+        } else {
+            for (int shift = kFastBits; shift < nbits; shift += kFastBits) {
+                fast_pass<EPL, false>(n, shift, key, ok, sl.K[cur], sl.V[cur], sl.K[cur ^ 1], sl.V[cur ^ 1], sl, false);
+                cur ^= 1;
+            }
+        }
+    }
+    PHASE(10);
+    // ---- segments: thread tid owns sorted entries [EPL*tid, EPL*tid + EPL)
+    const uint32_t* K = sl.K[cur];
+    const int32_t* Vs = sl.V[cur];
+    int32_t* sseg = sl.V[cur ^ 1];
+    uint32_t* srow = sl.K[cur ^ 1];
+    const int64_t off = (int64_t)t * ix.cap;
+    int32_t* perm = ix.perm + off;
+    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int i = tid + q * kFastThreads;
+        if (i < n) perm[i] = Vs[i];
+    }
+    int h = 0;
+    bool head[EPL];
+    uint32_t kq[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int i = EPL * tid + q;
+        kq[q] = i < n ? K[i] : 0u;
+        const uint32_t kp = (i > 0 && i < n) ? K[i - 1] : ~kq[q];
+        head[q] = i < n && kp != kq[q];
+        h += head[q] ? 1 : 0;
+    }
+    int U;
+    int s = block_scan_excl<int>(h, sl.wtot, &U);
+#pragma unroll
+    for (int q = 0; q < EPL; ++q)
+        if (head[q]) {
+            const int i = EPL * tid + q;
+            sseg[s] = i;
+            srow[s] = kq[q];
+            seg_start[s] = i;
+            seg_row[s] = kq[q];
+            ++s;
+        }
+    if (tid == 0) seg_start[U] = n;
+    __syncthreads();
+    PHASE(20);
+    // packed counts (N <= 4096 < 2^21): chunks bits 0-20, hot segments 21-41, hot slices 42-62
+    constexpr long long M21 = (1ll << 21) - 1;
+    long long cw = 0;
+    int beg[EPL], end[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int sidx = EPL * tid + q;
+        beg[q] = end[q] = 0;
+        if (sidx < U) {
+            beg[q] = sseg[sidx];
+            end[q] = sidx + 1 < U ? sseg[sidx + 1] : n;
+            const int len = end[q] - beg[q];
+            cw += len <= kChunk ? 1ll : ((1ll << 21) | ((long long)((len + kHotSlice - 1) / kHotSlice) << 42));
+        }
+    }
+    long long tot64;
+    const long long ex = block_scan_excl<long long>(cw, sl.wtot64, &tot64);
+    int c = (int)(ex & M21), hh = (int)((ex >> 21) & M21), ss = (int)((ex >> 42) & M21);
+    int4* chunks = ix.chunks + off;
+    int4* hot = ix.hot + off;
+    int32_t* hot_slice = ix.hot_slice + off;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int sidx = EPL * tid + q;
+        if (sidx < U) {
+            const int len = end[q] - beg[q];
+            if (len <= kChunk) {
+                chunks[c++] = make_int4(beg[q], end[q], (int)srow[sidx], Vs[beg[q]]);
+            } else {
+                const int ns = (len + kHotSlice - 1) / kHotSlice;
+                hot[hh] = make_int4(beg[q], end[q], (int)srow[sidx], ss);
+                for (int k = 0; k < ns; ++k) hot_slice[ss + k] = hh;
+                ++hh;
+                ss += ns;
+            }
+        }
+    }
+    if (tid == 0) {
+        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        cnt[CNT_U] = U; cnt[CNT_C] = (int)(tot64 & M21); cnt[CNT_H] = (int)((tot64 >> 21) & M21);
+        cnt[CNT_S] = (int)((tot64 >> 42) & M21); cnt[CNT_NV] = n;
+    }
+    PHASE(22);
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kFastThreads) void indexer_fast_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
+                                                                    const void* __restrict__ idx, int itype,
+                                                                    int64_t tstride, int base, int N,
+                                                                    unsigned* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    FastLds<EPL>& sl = *(FastLds<EPL>*)dyn;
+    const int t = blockIdx.x;
+#ifdef DLRM_PHASE
+    if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
+#endif
+    PHASE(0);
+    fast_index_table<EPL>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
+#ifdef DLRM_PHASE
+    if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
+#endif
 }
 
 // ------------------------------------------------------------------------------ apply
@@ -358,80 +690,249 @@ __device__ __forceinline__ void sum_positions(const int32_t* __restrict__ perm, 
 // chunk, no loop (the grid covers the worst case; idle groups exit).  Hot blocks: one
 // workgroup per hot segment; lane groups sum sub-chunks of `cs` positions into LDS, then
 // the partials are added in sub-chunk order and the row is written once.
-template <typename TT, typename GT, int VPR>
-__global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int L,
+// Hot segments: the 4*RPW lane groups of the workgroup take contiguous equal slices (size set
+// by the segment length only); each stages its slice's positions in LDS with one cooperative
+// read, then sums the grad rows in position order with kHotInFlight rows in flight.  The
+// group partials are added in group order and the row is written once.
+constexpr int kHotStage = 128;   // positions staged per lane group per round
+constexpr int kHotInFlight = 8;   // grad rows in flight per lane group
+
+template <typename GT, int VPR>
+__device__ __forceinline__ void sum_staged(const int32_t* stage, int m, int L, const GT* __restrict__ gbase,
+                                           int64_t grad_ld, int v,
+                                           float (&acc)[ApplyGeom<GT, VPR>::VPL][ApplyGeom<GT, VPR>::NE]) {
+    typedef ApplyGeom<GT, VPR> G;
+    typedef typename G::GV GV;
+    constexpr int IF = kHotInFlight / G::VPL;  // rows in flight (16-B vectors per lane bounded)
+    for (int i = 0; i < m; i += IF) {
+        typename GV::type gv[IF][G::VPL];
+#pragma unroll
+        for (int u = 0; u < IF; ++u)
+            if (i + u < m) {
+                const GT* gr = gbase + (int64_t)(stage[i + u] / L) * grad_ld;
+#pragma unroll
+                for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
+            }
+#pragma unroll
+        for (int u = 0; u < IF; ++u)
+            if (i + u < m) {
+#pragma unroll
+                for (int j = 0; j < G::VPL; ++j) {
+                    float f[G::NE];
+                    GV::to_f32(gv[u][j], f);
+#pragma unroll
+                    for (int e = 0; e < G::NE; ++e) acc[j][e] += f[e];
+                }
+            }
+    }
+}
+
+// Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
+// may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb, int key, int& table, int& local) {
+    // count of lanes with incl <= key (binary lifting over the non-decreasing prefix)
+    int pos = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const int vv = __shfl(incl, pos + step - 1, 64);
+        if (vv <= key) pos += step;
+    }
+    const int before = __shfl(incl, pos > 0 ? pos - 1 : 0, 64);
+    if (table < 0 && key >= 0 && key < tile_total) {
+        table = tb + pos;
+        local = key - (pos > 0 ? before : 0);
+    }
+}
+
+// Per-wave prefix of one count over the tables (T <= 64 kept in registers; more tables are
+// re-scanned tile by tile on every lookup).
+struct TableScan {
+    int incl;   // this lane's inclusive prefix (tile 0)
+    int total;  // over all tables
+};
+
+__device__ __forceinline__ TableScan scan_counts(const IndexerDev& ix, int T_, int which) {
+    const int lane = threadIdx.x & 63;
+    TableScan r{0, 0};
+    for (int tb = 0; tb < T_; tb += 64) {
+        const int tt = tb + lane;
+        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
+        const int incl = wave_incl_scan(c);
+        if (tb == 0) r.incl = incl;
+        r.total += __shfl(incl, 63, 64);
+    }
+    return r;
+}
+
+__device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, const TableScan& sc, int id,
+                                       int& table, int& local) {
+    table = -1;
+    local = 0;
+    if (T_ <= 64) {
+        locate_in_tile(sc.incl, sc.total, 0, id, table, local);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    int run = 0;
+    for (int tb = 0; tb < T_; tb += 64) {
+        const int tt = tb + lane;
+        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
+        const int incl = wave_incl_scan(c);
+        const int tot = __shfl(incl, 63, 64);
+        locate_in_tile(incl, tot, tb, id - run, table, local);
+        run += tot;
+    }
+}
+
+// Cross-workgroup hand-off of slice partials (cdna_hip_programming.md Guideline 16, R1):
+// payload stored write-through (sc1, agent-scope atomic stores), every storing wave drains
+// (vmcnt(0)) before the workgroup barrier, ONE lane adds to the segment's arrival counter;
+// the last arriver reads every partial with sc1 loads (no acquire needed) and resets the
+// counter for the next launch.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+__device__ __forceinline__ void store_sc1(float* p, const f32x4& v) {
+    const unsigned long long lo = ((unsigned long long)__float_as_uint(v[1]) << 32) | __float_as_uint(v[0]);
+    const unsigned long long hi = ((unsigned long long)__float_as_uint(v[3]) << 32) | __float_as_uint(v[2]);
+    __hip_atomic_store((gu64_t*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64_t*)(p + 2), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ f32x4 load_sc1(const float* p) {
+    const unsigned long long lo = __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load((gu64_t*)(p + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return f32x4{__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)), __uint_as_float((uint32_t)hi),
+                 __uint_as_float((uint32_t)(hi >> 32))};
+}
+
+template <typename TT>
+__device__ __forceinline__ void sgd_row4(TT* row, int c0, const f32x4& sum, float lr) {
+    float f[4];
+    load_row<TT, 4>(row, c0, f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = __builtin_fmaf(-lr, sum[e], f[e]);
+    store_row<TT, 4>(row, c0, f);
+}
+
+// Persistent launch, flat over tables.  Work items: [0, S) = the S slices of every table's hot
+// segments (kHotSlice positions, one workgroup each, handed out first), then ceil(C / NG)
+// items of NG chunks (one per lane group).  Workgroup b takes items b, b + grid, ...: every
+// item is short, so static striding balances, and no workgroup is launched past the work.
+template <typename TT, typename GT, int VPR, int CPG>
+__global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_, int L,
                                                         const GT* __restrict__ grad, int64_t grad_ld,
-                                                        int64_t grad_offset, float lr, int chunk_blocks,
-                                                        int hot_chunks_max) {
+                                                        int64_t grad_offset, float lr) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE;
     constexpr int D = G::D;
-    extern __shared__ __attribute__((aligned(16))) float hot_part[];  // [hot_chunks_max][D]
-    const int t = blockIdx.y;
+    constexpr int NG = 4 * G::RPW;                      // lane groups per workgroup
+    constexpr int PER = (kHotSlice + NG - 1) / NG;       // positions of a slice per lane group
+    __shared__ __attribute__((aligned(16))) float hot_part[NG][D];  // <= 8 KB
+    __shared__ int32_t hot_stage[NG][PER];
+    __shared__ int sh_last;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane / G::LPR, v = lane % G::LPR;
-    const int64_t off = (int64_t)t * ix.cap;
-    const int32_t* perm = ix.perm + off;
-    const GT* gbase = grad + grad_offset + (int64_t)t * D;
-    TT* table = (TT*)tabs[t].data;
-    if ((int)blockIdx.x < chunk_blocks) {
-        if (g >= G::RPW) return;
-        const int cid = (blockIdx.x * (blockDim.x >> 6) + w) * G::RPW + g;
-        if (cid >= ix.counts[(int64_t)t * 8 + CNT_C]) return;
-        const int4 cd = ix.chunks[off + cid];
-        TT* row = table + (int64_t)(uint32_t)cd.z * D;
-        float tv[G::VPL][NE];  // the table row, loaded while the grad rows stream in
+    const int gid = w * G::RPW + g;
+    const TableScan sS = scan_counts(ix, T_, CNT_S);
+    const TableScan sC = scan_counts(ix, T_, CNT_C);
+    const int items = sS.total + (sC.total + NG - 1) / NG;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        APPLY_START(item >= sS.total ? 1 : 2);
+        if (item >= sS.total) {
+            // ---- NG chunks: one per lane group (table row prefetched while the grad rows of
+            // its positions stream in, summed in ascending position order)
+            int tc, cl;
+            locate(ix, T_, CNT_C, sC, (item - sS.total) * NG + gid, tc, cl);
+            if (g >= G::RPW || tc < 0) continue;
+            const int64_t off = (int64_t)tc * ix.cap;
+            const GT* gbase = grad + grad_offset + (int64_t)tc * D;
+            const int4 cd = ix.chunks[off + cl];
+            TT* row = (TT*)tabs[tc].data + (int64_t)(uint32_t)cd.z * D;
+            float tv[G::VPL][NE];
 #pragma unroll
-        for (int j = 0; j < G::VPL; ++j) load_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
-        float acc[G::VPL][NE];
-#pragma unroll
-        for (int j = 0; j < G::VPL; ++j)
-#pragma unroll
-            for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-        sum_positions<GT, VPR>(perm, cd.x, cd.y, L, gbase, grad_ld, v, acc, cd.w);
-#pragma unroll
-        for (int j = 0; j < G::VPL; ++j) {
-#pragma unroll
-            for (int e = 0; e < NE; ++e) tv[j][e] = __builtin_fmaf(-lr, acc[j][e], tv[j][e]);
-            store_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
-        }
-        return;
-    }
-    // ---- hot segment
-    const int h = blockIdx.x - chunk_blocks;
-    if (h >= ix.counts[(int64_t)t * 8 + CNT_H]) return;
-    const int4 hd = ix.hot[off + h];
-    const int n = hd.y - hd.x;
-    const int cs = max(kChunk, (n + hot_chunks_max - 1) / hot_chunks_max);  // depends on n only
-    const int nch = (n + cs - 1) / cs;
-    const int groups = (blockDim.x >> 6) * G::RPW;
-    if (g < G::RPW) {
-        for (int c = w * G::RPW + g; c < nch; c += groups) {
+            for (int j = 0; j < G::VPL; ++j) load_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
             float acc[G::VPL][NE];
 #pragma unroll
             for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
                 for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-            const int b0 = hd.x + c * cs;
-            sum_positions<GT, VPR>(perm, b0, min(b0 + cs, hd.y), L, gbase, grad_ld, v, acc);
+            sum_positions<GT, VPR>(ix.perm + off, cd.x, cd.y, L, gbase, grad_ld, v, acc, cd.w);
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j) {
+#pragma unroll
+                for (int e = 0; e < NE; ++e) tv[j][e] = __builtin_fmaf(-lr, acc[j][e], tv[j][e]);
+                store_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
+            }
+            APPLY_END();
+            continue;
+        }
+        // ---- one slice of a hot segment: lane groups sum contiguous parts, in group order
+        int th, sl;
+        locate(ix, T_, CNT_S, sS, item, th, sl);  // item < S: found, the same for every lane
+        const int64_t off = (int64_t)th * ix.cap;
+        const int hseg = ix.hot_slice[off + sl];
+        const int4 hd = ix.hot[off + hseg];
+        const int ns = (hd.y - hd.x + kHotSlice - 1) / kHotSlice;
+        const int p0 = hd.x + (sl - hd.w) * kHotSlice, p1 = min(p0 + kHotSlice, hd.y);
+        {
+            float acc[G::VPL][NE];
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j)
+#pragma unroll
+                for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
+            const int b0 = min(p0 + gid * PER, p1), m = min(b0 + PER, p1) - b0;
+            const int32_t* perm = ix.perm + off;
+            int32_t* stage = hot_stage[gid];
+            for (int k = v; k < m; k += G::LPR) stage[k] = perm[b0 + k];
+            wave_lds_sync();
+            sum_staged<GT, VPR>(stage, m, L, grad + grad_offset + (int64_t)th * D, grad_ld, v, acc);
 #pragma unroll
             for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
                 for (int e = 0; e < NE; e += 4)
-                    *(f32x4*)(hot_part + (int64_t)c * D + (v + j * 64) * NE + e) =
+                    *(f32x4*)(&hot_part[gid][(v + j * 64) * NE + e]) =
                         f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
         }
-    }
-    __syncthreads();
-    TT* row = table + (int64_t)(uint32_t)hd.z * D;
-    for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
-        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int c = 0; c < nch; ++c) s += *(const f32x4*)(hot_part + (int64_t)c * D + c0);
-        float f[4];
-        load_row<TT, 4>(row, c0, f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) f[e] = __builtin_fmaf(-lr, s[e], f[e]);
-        store_row<TT, 4>(row, c0, f);
+        __syncthreads();
+        TT* row = (TT*)tabs[th].data + (int64_t)(uint32_t)hd.z * D;
+        float* part = ix.partial + ((int64_t)th * ix.pcap + sl) * ix.pdim;
+        for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
+            f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < NG; ++c) sum += *(const f32x4*)(&hot_part[c][c0]);
+            if (ns == 1) sgd_row4<TT>(row, c0, sum, lr);
+            else store_sc1(part + c0, sum);
+        }
+        if (ns > 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+            __syncthreads();
+            if (threadIdx.x == 0)
+                sh_last = __hip_atomic_fetch_add((gi32_t*)(ix.hot_cnt + off + hseg), 1, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
+            __syncthreads();
+            if (sh_last) {
+                const float* first = ix.partial + ((int64_t)th * ix.pcap + hd.w) * ix.pdim;
+                for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
+                    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int k = 0; k < ns; ++k) sum += load_sc1(first + (int64_t)k * ix.pdim + c0);
+                    sgd_row4<TT>(row, c0, sum, lr);
+                }
+                if (threadIdx.x == 0)
+                    __hip_atomic_store((gi32_t*)(ix.hot_cnt + off + hseg), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();  // hot_part / hot_stage / sh_last reused by this workgroup's next item
+        APPLY_END();
     }
 }
 
@@ -508,36 +1009,44 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-    if (N <= kLdsSortMax)
-        hipLaunchKernelGGL(indexer_build_kernel<true>, dim3(T_), dim3(kBuildThreads), indexer_lds_bytes(), s, ix, tabs,
-                           idx, itype, tstride, base, B, L, ctx_error_word(ctx));
-    else
+    if (N <= kFastThreads * 2) {
+        hipLaunchKernelGGL(indexer_fast_kernel<2>, dim3(T_), dim3(kFastThreads), sizeof(FastLds<2>), s, ix, tabs, idx,
+                           itype, tstride, base, (int)N, ctx_error_word(ctx));
+    } else if (N <= kFastMaxN) {
+        static const hipError_t a4 = hipFuncSetAttribute((const void*)indexer_fast_kernel<4>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                         (int)sizeof(FastLds<4>));
+        (void)a4;
+        hipLaunchKernelGGL(indexer_fast_kernel<4>, dim3(T_), dim3(kFastThreads), sizeof(FastLds<4>), s, ix, tabs, idx,
+                           itype, tstride, base, (int)N, ctx_error_word(ctx));
+    } else
         hipLaunchKernelGGL(indexer_build_kernel<false>, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, idx, itype,
                            tstride, base, B, L, ctx_error_word(ctx));
     return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
-}
-
-// hot-segment partials per workgroup: 16 sub-chunks up to D = 256 (<= 16 KB of LDS, so the
-// chunk blocks of the same launch keep their occupancy), fewer beyond
-static int hot_chunks_for(int D) {
-    const int n = 4096 / D;
-    return n > kHotChunksMax ? kHotChunksMax : (n < 4 ? 4 : n);
 }
 
 template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
                              int64_t grad_ld, int64_t grad_offset, float lr, int64_t N) {
     typedef ApplyGeom<GT, VPR> G;
-    const int per_block = 4 * G::RPW;     // 4 waves x RPW lane groups, one chunk each
-    const int64_t cb = (N + per_block - 1) / per_block;
-    const int64_t hb = N / (kChunk + 1);  // at most this many segments longer than kChunk
-    const int hc = hot_chunks_for(G::D);
-    const size_t lds = sizeof(float) * (size_t)hc * G::D;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)attr;
-    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR>), dim3((unsigned)(cb + hb < 1 ? 1 : cb + hb), T_), dim3(256),
-                       lds, s, ix, tabs, L, (const GT*)grad, grad_ld, grad_offset, lr, (int)cb, hc);
+    constexpr int CPG = 1;                   // chunks per lane group (4 measured slower)
+    const int per_block = 4 * G::RPW * CPG;  // 4 waves x RPW lane groups x CPG chunks
+    // persistent grid: resident workgroups only (never more than the worst-case item count)
+    const int64_t cb = ((int64_t)T_ * N + per_block - 1) / per_block;
+    const int64_t hb = (int64_t)T_ * (N / (kChunk + 1));
+    static int per_cu = 0;
+    if (!per_cu) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR, CPG>, 256, 0) !=
+                hipSuccess || per_cu < 1)
+            per_cu = 4;
+    }
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int64_t grid = (int64_t)per_cu * (cus > 0 ? cus : 256);
+    if (grid > cb + hb) grid = cb + hb;
+    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, CPG>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(256), 0, s,
+                       ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr);
 }
 
 template <typename TT, typename GT>
@@ -562,7 +1071,8 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     const bool aligned = tabs_aligned16 && (uintptr_t)grad % 16 == 0 && (grad_ld * gesz) % 16 == 0 &&
                          (grad_offset * gesz) % 16 == 0 && (D * gesz) % 16 == 0 && (D * tesz) % 16 == 0 && D % 4 == 0;
     bool done = false;
-    if (aligned) {
+    const int64_t slots = (int64_t)T_ * ((N + 7) / 8 + N / (kChunk + 1));  // launch_apply_vec's grid bound
+    if (aligned && slots < (1ll << 31)) {
         const int vpr = D * gesz / 16;
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
             done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N);

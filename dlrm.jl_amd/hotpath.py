@@ -9,12 +9,19 @@ does for the sparse half of the model on one batch:
     dx, dt = dot_back(dot, dout, T, d, padding)                    interact.jl:442-445
     update!(Descent(lr), tables, maplookup_pullback(dt), indexers) train.jl:283-290
 
-All buffers are allocated once; a step issues 5 kernel launches on the current stream
-(fused lookup + interaction fwd, indexer sort, interaction bwd, 2 for the update) with no
-host synchronisation, so the whole step can be captured in a torch.cuda graph
-(`fused=False` runs maplookup and the interaction as two launches, like the reference).  With
-`overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a
-side stream concurrently with the lookup and the interaction.
+All buffers are allocated once; a step issues 4 kernel launches on the current stream
+(fused lookup + interaction fwd, indexer sort, interaction bwd, update) with no host
+synchronisation, so the whole step can be captured in a torch.cuda graph (`fused=False`
+runs maplookup and the interaction as two launches, like the reference).  With
+`overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a side
+stream concurrently with the lookup and the interaction.
+
+`materialize_ys` (default: off wherever it applies, i.e. fused forward and one-hot lookups):
+the reference keeps the lookup output ys (= the interaction's T) for dot_back.  Off, the
+forward writes only `out` and the backward rebuilds T from x and the gathered table rows
+(dlrm_interact_bwd_gather) -- the same values, bit for bit, since the tables change only in
+the update that follows -- which saves ys's write and keeps the step's HBM traffic at what
+the math needs.  Turn it on to read `ys` (e.g. for parity checks against maplookup).
 """
 import torch
 
@@ -27,7 +34,7 @@ from .update import SparseIndexer
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=False, pad_to=1, fused=True):
+                 overlap_indexer=False, pad_to=1, fused=True, materialize_ys=None):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -39,7 +46,14 @@ class HotPath:
         self.fused = fused
         _, self.width, self.padding = interaction_sizes(self.d, self.F, pad_to)
         dev, dt = self.ts.device, self.ts.dtype
-        self.ys = torch.empty((self.B, self.F * self.D), dtype=dt, device=dev)
+        can_skip = fused and self.L == 1
+        if materialize_ys is None:
+            materialize_ys = not can_skip
+        if not materialize_ys and not can_skip:
+            raise ValueError("materialize_ys=False needs the fused forward and one-hot lookups (lookups=1)")
+        self.materialize_ys = bool(materialize_ys)
+        self.ys = torch.empty((self.B, self.F * self.D), dtype=dt, device=dev) if self.materialize_ys else None
+        self._fwd_x = self._fwd_idx = None
         self.out = torch.empty((self.B, self.width), dtype=dt, device=dev)
         self.dx = torch.empty((self.B, self.d), dtype=torch.float32, device=dev)
         self.dt = torch.empty((self.B, self.F * self.d), dtype=torch.float32, device=dev)
@@ -69,21 +83,34 @@ class HotPath:
 
     def lookup_interact_fwd(self, x, idx):
         h = self.ctx.bind()
+        ys, ys_ld = (ptr(self.ys), self.ys.stride(0)) if self.materialize_ys else (None, 0)
         self._check(self.lib.dlrm_lookup_interact_fwd(h, self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
-                                                      self.index_base, self.B, self.L, ptr(x), x.stride(0),
-                                                      ptr(self.ys), self.ys.stride(0), ptr(self.out),
-                                                      self.out.stride(0), self.padding))
+                                                      self.index_base, self.B, self.L, ptr(x), x.stride(0), ys,
+                                                      ys_ld, ptr(self.out), self.out.stride(0), self.padding))
+        self._fwd_x, self._fwd_idx = x, idx
 
     def build_indexer(self, idx):
         h = self.ctx.bind()
         self._check(self.lib.dlrm_indexer_build(h, self.indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
                                                 idx.stride, self.index_base, self.B, self.L))
 
-    def interact_bwd(self, dout):
+    def interact_bwd(self, dout, x=None, idx=None):
+        """dot_back.  Without a materialized ys, T is rebuilt from x and the indices of the
+        forward (the last forward's unless given)."""
         h = self.ctx.bind()
-        self._check(self.lib.dlrm_interact_bwd(h, self.dcode, self.d, self.F, self.B, ptr(dout), dout.stride(0),
-                                               self.padding, ptr(self.ys), self.ys.stride(0), ptr(self.dx),
-                                               self.dx.stride(0), ptr(self.dt), self.dt.stride(0)))
+        if self.materialize_ys:
+            self._check(self.lib.dlrm_interact_bwd(h, self.dcode, self.d, self.F, self.B, ptr(dout), dout.stride(0),
+                                                   self.padding, ptr(self.ys), self.ys.stride(0), ptr(self.dx),
+                                                   self.dx.stride(0), ptr(self.dt), self.dt.stride(0)))
+            return
+        x = self._fwd_x if x is None else x
+        idx = self._fwd_idx if idx is None else idx
+        if x is None or idx is None:
+            raise RuntimeError("interact_bwd without a materialized ys needs the forward's x and indices")
+        self._check(self.lib.dlrm_interact_bwd_gather(h, self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
+                                                      self.index_base, self.B, self.L, ptr(x), x.stride(0),
+                                                      ptr(dout), dout.stride(0), self.padding, ptr(self.dx),
+                                                      self.dx.stride(0), ptr(self.dt), self.dt.stride(0)))
 
     def sgd_update(self, idx, prebuilt):
         h = self.ctx.bind()
@@ -125,7 +152,7 @@ class HotPath:
         return self.out
 
     def backward(self, idx, dout):
-        self.interact_bwd(dout)
+        self.interact_bwd(dout, idx=idx)
         prebuilt = False
         if self.overlap_indexer and self._indexer_done is not None:
             torch.cuda.current_stream(self.ts.device).wait_event(self._indexer_done)

@@ -121,7 +121,9 @@ int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
  * loaded once into MFMA fragments and written to ys from registers, so ys is never re-read.
  * ys and out receive exactly what dlrm_maplookup(out_offset = d) + dlrm_interact_fwd write
  * (bit-identical); shapes without a fused kernel fall back to those two launches.
- * Requires tables->dim == d; dtype is the tables' dtype. */
+ * ys may be NULL when the caller will not read the lookup output (a training step whose
+ * backward is dlrm_interact_bwd_gather): then only out is written, and shapes without a
+ * fused kernel return DLRM_E_UNSUPPORTED.  Requires tables->dim == d; dtype is the tables'. */
 int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tables,
                              const void* indices, int itype, int64_t table_stride, int index_base,
                              int batch, int lookups,
@@ -136,6 +138,16 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
                       const void* dout, int64_t dout_ld, int padding,
                       const void* t, int64_t t_ld,
                       float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
+
+/* dot_back as dlrm_interact_bwd, with T_b rebuilt from x (row 0) and the tables' rows of the
+ * sample's one-hot indices (rows 1..F-1) instead of read from a materialized ys: the same
+ * values while the tables are unchanged since the forward (recomputation, not a cache).
+ * lookups must be 1; dtype is the tables' (dout and x in it); dx, dt fp32 as above. */
+int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tables,
+                             const void* indices, int itype, int64_t table_stride, int index_base,
+                             int batch, int lookups, const void* x, int64_t x_ld,
+                             const void* dout, int64_t dout_ld, int padding,
+                             float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 
 /* ---- sparse indexer + SGD scatter update --------------------------------------------- */
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_table,

@@ -303,8 +303,10 @@ def test_update_bounds_error(pkg, gpu):
 
 
 # ------------------------------------------------------------------ the engine
-@pytest.mark.parametrize("overlap", [False, True])
-def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap):
+@pytest.mark.parametrize("overlap,materialize", [(False, False), (False, True), (True, False), (True, True)])
+def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap, materialize):
+    """The engine (fused forward; backward from a materialized ys or re-gathered rows) equals
+    the reference-shaped operator sequence bit for bit."""
     rng = np.random.default_rng(1)
     rows = [10, 3000, 7, 100000]
     D, B = 32, 512
@@ -314,7 +316,7 @@ def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap):
     F = len(rows) + 1
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu)
     hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0,
-                     overlap_indexer=overlap)
+                     overlap_indexer=overlap, materialize_ys=materialize)
     p = pkg.PackedIndices(idx)
     hp.step(x, p, dout)
     torch.cuda.synchronize()
@@ -327,6 +329,7 @@ def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap):
     pkg.update_(pkg.Descent(0.25), ts2, pkg.maplookup_pullback(D, ts2, p, dy), index_base=0)
     assert np.array_equal(to_np_f32(hp.out), to_np_f32(out))
     assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
+    assert np.array_equal(to_np_f32(hp.dt), to_np_f32(dy))
     for a, b in zip(hp.ts, ts2):
         assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
 
@@ -388,7 +391,7 @@ def test_fused_lookup_interaction_equals_two_operators(pkg, gpu, rows, D, B, L, 
     tabs = dev_tables(rand_tables(rng, rows, D), gpu, dtype)
     idx = torch.from_numpy(rand_indices(rng, rows, B, L)).reshape(len(rows), B, L).to(torch.int32).to(gpu)
     x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
-    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), B, L, index_base=0, fused=True)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), B, L, index_base=0, fused=True, materialize_ys=True)
     p = pkg.PackedIndices(idx)
     hp.validate(x, p)
     hp.forward(x, p)
@@ -402,12 +405,24 @@ def test_fused_lookup_interaction_equals_two_operators(pkg, gpu, rows, D, B, L, 
 
 def test_fused_bounds_error(pkg, gpu):
     tabs = [torch.ones((4, 16), device=gpu), torch.ones((4, 16), device=gpu)]
-    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), 2, 1, index_base=0)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), 2, 1, index_base=0, materialize_ys=True)
     x = torch.zeros((2, 16), device=gpu)
     hp.forward(x, pkg.PackedIndices(torch.tensor([[0, 1], [2, 4]], dtype=torch.int32, device=gpu)))
     with pytest.raises(pkg.BoundsError):
         hp.check_bounds()
     assert torch.equal(hp.ys[0, 16:], torch.ones(32, device=gpu))  # valid rows still gathered
+
+
+def test_gather_backward_bounds_error(pkg, gpu):
+    """The re-gathering backward validates indices like the forward (BoundsError, no fault)."""
+    tabs = [torch.ones((4, 16), device=gpu), torch.ones((4, 16), device=gpu)]
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(tabs), 2, 1, index_base=0)
+    assert not hp.materialize_ys
+    x = torch.zeros((2, 16), device=gpu)
+    bad = pkg.PackedIndices(torch.tensor([[0, 1], [2, 7]], dtype=torch.int32, device=gpu))
+    hp.interact_bwd(torch.zeros((2, hp.width), device=gpu), x=x, idx=bad)
+    with pytest.raises(pkg.BoundsError):
+        hp.check_bounds()
 
 
 def test_host_tensors_are_rejected_before_launch(pkg, gpu):

@@ -24,8 +24,7 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1)))
     rows.sort()
     # a step starts at each fused-forward / lookup kernel
-    starts = [i for i, r in enumerate(rows) if r[2] in ("interact_fwd_kernel", "maplookup_vec", "indexer_pack_kernel",
-                                                      "indexer_build_kernel")]
+    starts = [i for i, r in enumerate(rows) if r[2] in ("interact_fwd_kernel", "maplookup_vec", "indexer_build_kernel")]
     firsts = []
     for i in starts:
         if not firsts or rows[i][0] - rows[firsts[-1]][0] > 20000:
