@@ -276,7 +276,19 @@ def main():
             engine.sgd_update(packs[k], prebuilt=True)
             engine.indexer = home
 
-        if engine.fused:
+        in_bwd = (engine.fused and not engine.materialize_ys and engine.indexer is not None
+                  and not engine.overlap_indexer)
+
+        def bwd_index_k(k):
+            engine.indexer = indexers[k]
+            engine.interact_bwd(dout, x=x, idx=packs[k], build_indexer=True)
+            engine.indexer = home
+
+        if in_bwd:  # the indexer is built inside the backward's launch
+            names = ["lookup_interact_fwd", "interact_bwd", "sgd_update"]
+            fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), bwd_index_k, apply_k]
+            bytes_["interact_bwd"] += bytes_["indexer_build"]
+        elif engine.fused:
             names = ["lookup_interact_fwd", "indexer_build", "interact_bwd", "sgd_update"]
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: engine.build_indexer(packs[k]),
                    lambda k: engine.interact_bwd(dout, x=x, idx=packs[k]), apply_k]

@@ -61,8 +61,8 @@ SIGNATURES = {
     "dlrm_lookup_interact_fwd": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64,
                                          _i32]),
     "dlrm_interact_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp, _i64]),
-    "dlrm_interact_bwd_gather": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp,
-                                        _i64, _vp, _i64]),
+    "dlrm_interact_bwd_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _i32,
+                                        _vp, _i64, _vp, _i64]),
     "dlrm_indexer_create": (_i32, [_vp, _i32, _i64, _pp]),
     "dlrm_indexer_destroy": (_i32, [_vp]),
     "dlrm_indexer_build": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32]),

@@ -279,7 +279,7 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
     return launch_interact_bwd(ctx, dtype, d, num_features, batch, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
 }
 
-int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
+int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
                              int64_t table_stride, int index_base, int batch, int lookups, const void* x,
                              int64_t x_ld, const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld,
                              float* dt, int64_t dt_ld) {
@@ -293,8 +293,24 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, const void* i
     CHECK_ARG(padding >= 0 && x_ld >= d && dout_ld >= d + P + padding && dx_ld >= d && dt_ld >= (int64_t)F * d,
               "dlrm_interact_bwd_gather: leading dimensions too small");
     CHECK_ARG(batch == 0 || (x && dout && dx && dt), "dlrm_interact_bwd_gather: null buffer");
-    return launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
-                                      index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld);
+    if (ix) {
+        CHECK_ARG(tb->T == ix->T, "dlrm_interact_bwd_gather: indexer has %d tables, tables has %d", ix->T, tb->T);
+        CHECK_ARG((int64_t)batch * lookups <= ix->dev.cap,
+                  "dlrm_interact_bwd_gather: batch*lookups %lld > indexer capacity %lld", (long long)batch * lookups,
+                  (long long)ix->dev.cap);
+    }
+    rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                    index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld,
+                                    ix ? &ix->dev : nullptr);
+    if (rc || !ix) return rc;
+    ix->built = true;  // as dlrm_indexer_build: a following update may pass DLRM_UPDATE_PREBUILT
+    ix->indices = indices;
+    ix->itype = itype;
+    ix->tstride = table_stride;
+    ix->base = index_base;
+    ix->B = batch;
+    ix->L = lookups;
+    return DLRM_OK;
 }
 
 // --------------------------------------------------------------------------- indexer

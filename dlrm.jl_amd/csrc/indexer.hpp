@@ -1,0 +1,383 @@
+// indexer.hpp — the in-LDS SparseIndexer build (one workgroup per table, N <= 4096 positions),
+// shared by the standalone indexer launch (update.hip) and the backward launch that builds the
+// indexer in the same grid (interact.hip).  See update.hip for the apply that consumes it.
+#pragma once
+#include "common.hpp"
+
+#ifndef PHASE
+#define PHASE(k) do {} while (0)
+#endif
+
+namespace dlrm {
+
+constexpr int kChunk = 32;          // max positions of a segment handled by one lane group
+constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
+enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
+// Hot segments are cut into slices of kHotSlice positions, one work item each; a segment of
+// several slices is combined by its last-arriving slice (sc1 partial rows + a counter).
+constexpr int kHotSlice = 128;
+
+// Exclusive scan over the NW waves' 64*NW threads; returns this thread's prefix, total in *tot.
+template <int NW, typename V>
+__device__ __forceinline__ V block_scan_nw(V v, V* wtot, V* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    V x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const V y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        V t = lane < NW ? wtot[lane] : V(0);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const V y = __shfl_up(t, off, 64);
+            if (lane >= off) t += y;
+        }
+        if (lane < NW) wtot[NW + lane] = t;  // inclusive wave totals
+    }
+    __syncthreads();
+    const V before = w ? wtot[NW + w - 1] : V(0);
+    *tot = wtot[2 * NW - 1];
+    __syncthreads();  // wtot reusable after return
+    return before + x - v;
+}
+
+// ------------------------------------------------------------------- fast indexer (N <= 4096)
+// One 1024-thread workgroup per table; everything stays in LDS.
+//  * Stable counting pass on an 8-bit digit: wave w walks positions [w*S, (w+1)*S) (S = 64*EPL)
+//    in tiles of 64, so "earlier position" = earlier wave, earlier tile or lower lane.  Lanes
+//    sharing a digit are found with 8 ballots; each wave keeps its running count of every
+//    digit in its own column of cnt[digit][wave] (only that wave touches it, in program
+//    order), which gives each key its rank among the wave's earlier equal digits.  One block
+//    scan over cnt in (digit, wave) order turns the counts into output offsets: no serial
+//    cross-wave loop.  Invalid indices are dropped (they raised the bounds flag).
+//  * Rows of <= 8 bits are then grouped.  Larger rows: when every bucket is small (uniform
+//    rows: N/256 keys per bucket) each bucket is ordered by a direct rank on (row, position);
+//    skewed rows take the remaining LSD passes.
+//  * Segments and the chunk / hot lists: one head-flag scan and one packed 64-bit scan.
+// Output format = indexer_build_kernel's (the apply kernel and dlrm_indexer_read unchanged).
+constexpr int kFastMaxN = 4096;
+
+// NT threads (1024 standalone; 256 inside the backward launch), EPL positions per thread.
+// Digit width: 8 bits with 16 waves, 11 bits with 4 (about one key per bucket at N = 2048, so
+// the within-bucket rank is short where one wave per SIMD hides no latency).
+template <int NT, int EPL>
+struct FastLds {
+    static constexpr int NW = NT / 64;
+    static constexpr int DB = NT >= 1024 ? 8 : 11;  // digit bits
+    static constexpr int ND = 1 << DB;              // digits
+    static constexpr int CPT = ND * NW / NT;        // (digit, wave) counters per thread: 4 or 32
+    static_assert(CPT == 4 || CPT % 8 == 0, "counters per thread: 4, or whole uint4s");
+    uint16_t cnt[ND][NW];       // digit-major: per-wave counts, then output offsets
+    uint16_t bstart[ND + 8];    // first-pass bucket starts
+    uint32_t K[2][NT * EPL];
+    int32_t V[2][NT * EPL];
+    int wtot[2 * NW];
+    long long wtot64[2 * NW];
+    int maxbucket;
+};
+
+// One stable counting pass.  FROM_REGS: the first pass's keys come from registers (tile j
+// of wave w = position w*S + 64j + lane); otherwise from kin/vin[0, n) in LDS.  Returns the
+// number of keys written to kout/vout.
+template <int NT, int EPL, bool FROM_REGS>
+__device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bool (&rok)[EPL],
+                         const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
+                         FastLds<NT, EPL>& sl, bool first) {
+    typedef FastLds<NT, EPL> FL;
+    constexpr int CPT = FL::CPT, NW = FL::NW;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    constexpr int S = 64 * EPL;
+    if (CPT == 4) {
+        ((uint2*)&sl.cnt[0][0])[tid] = make_uint2(0, 0);
+    } else {
+#pragma unroll
+        for (int k = 0; k < CPT / 8; ++k) ((uint4*)&sl.cnt[0][0])[tid * (CPT / 8) + k] = make_uint4(0, 0, 0, 0);
+    }
+    uint32_t key[EPL];
+    int32_t val[EPL];
+    bool ok[EPL];
+    int lr[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        if (FROM_REGS) {
+            key[j] = rkey[j];
+            ok[j] = rok[j];
+            val[j] = i;
+        } else {
+            ok[j] = i < n;
+            key[j] = ok[j] ? kin[i] : 0u;
+            val[j] = ok[j] ? vin[i] : 0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const uint32_t d = (key[j] >> shift) & (FL::ND - 1);
+        unsigned long long peers = __ballot(ok[j]);
+#pragma unroll
+        for (int bit = 0; bit < FL::DB; ++bit) {
+            const unsigned long long bb = __ballot(ok[j] && ((d >> bit) & 1u));
+            peers &= ((d >> bit) & 1u) ? bb : ~bb;
+        }
+        int base = 0;
+        if (ok[j] && j > 0) base = sl.cnt[d][w];
+        lr[j] = base + __popcll(peers & lt);
+        if (ok[j] && (peers & lt) == 0) sl.cnt[d][w] = (uint16_t)(base + __popcll(peers));
+    }
+    __syncthreads();
+    // (digit, wave) offsets: thread tid owns the CPT counters [CPT tid, CPT tid + CPT) of cnt
+    // in (digit, wave) order; one block scan over the per-thread sums
+    uint32_t cw[CPT / 2];  // CPT uint16 counters, two per word
+    if (CPT == 4) {
+        const uint2 r = ((const uint2*)&sl.cnt[0][0])[tid];
+        cw[0] = r.x;
+        cw[1] = r.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < CPT / 8; ++k) {
+            const uint4 r = ((const uint4*)&sl.cnt[0][0])[tid * (CPT / 8) + k];
+            cw[4 * k] = r.x; cw[4 * k + 1] = r.y; cw[4 * k + 2] = r.z; cw[4 * k + 3] = r.w;
+        }
+    }
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < CPT / 2; ++k) sum += (int)(cw[k] & 0xffffu) + (int)(cw[k] >> 16);
+    int total;
+    const int ex = block_scan_nw<NW, int>(sum, sl.wtot, &total);
+    {
+        int run = ex;
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+            const int e = CPT * tid + k;  // counter e = (digit e / NW, wave e % NW)
+            const int c = (int)((cw[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+            if (first && e % NW == 0) sl.bstart[e / NW] = (uint16_t)run;
+            if (k & 1) cw[k >> 1] = (cw[k >> 1] & 0xffffu) | ((uint32_t)run << 16);
+            else cw[k >> 1] = (cw[k >> 1] & 0xffff0000u) | (uint32_t)run;
+            run += c;
+        }
+    }
+    if (CPT == 4) {
+        ((uint2*)&sl.cnt[0][0])[tid] = make_uint2(cw[0], cw[1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < CPT / 8; ++k)
+            ((uint4*)&sl.cnt[0][0])[tid * (CPT / 8) + k] = make_uint4(cw[4 * k], cw[4 * k + 1], cw[4 * k + 2], cw[4 * k + 3]);
+    }
+    if (first && tid == 0) {
+        sl.bstart[FL::ND] = (uint16_t)total;
+        sl.maxbucket = 0;
+    }
+    __syncthreads();
+    if (first) {
+        // largest bucket (decides rank sort vs more passes)
+        int m = 0;
+        for (int dd = tid; dd < FL::ND; dd += NT) m = max(m, (int)sl.bstart[dd + 1] - (int)sl.bstart[dd]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if (lane == 0 && m > 0) atomicMax(&sl.maxbucket, m);
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j)
+        if (ok[j]) {
+            const uint32_t d = (key[j] >> shift) & (FL::ND - 1);
+            const int dst = sl.cnt[d][w] + lr[j];
+            kout[dst] = key[j];
+            vout[dst] = val[j];
+        }
+    __syncthreads();
+    return total;
+}
+
+template <int NT, int EPL>
+__device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, const void* __restrict__ idx,
+                                 int itype, int64_t tstride, int base, int N, unsigned* __restrict__ err,
+                                 FastLds<NT, EPL>& sl) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int S = 64 * EPL;
+    const int nbits = 32 - __clz(nrows > 0 ? nrows - 1 : 0);
+    // the indices, read once (coalesced 64-lane runs, all loads in flight) and validated
+    uint32_t key[EPL];
+    bool ok[EPL];
+    int64_t raw[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        raw[j] = load_index(idx, itype, t * tstride + min(i, N - 1));
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int i = w * S + j * 64 + lane;
+        const int64_t r = raw[j] - base;
+        ok[j] = i < N && r >= 0 && r < (int64_t)nrows;
+        key[j] = ok[j] ? (uint32_t)r : 0u;
+        if (i < N && !ok[j]) raise_index_error(err);
+    }
+    PHASE(1);
+    const int n = fast_pass<NT, EPL, true>(N, 0, key, ok, nullptr, nullptr, sl.K[1], sl.V[1], sl, true);
+    PHASE(5);
+    int cur = 1;
+    typedef FastLds<NT, EPL> FL;
+    if (nbits > FL::DB) {
+        if (sl.maxbucket <= kRankBucketMax) {
+            // order each bucket by (row, position); the stable pass kept positions ascending
+            if (FL::DB >= 11) {
+                // ~1 key per bucket: issue every key's loads together (EPL in flight) rather
+                // than one dependent chain per key
+                uint32_t ki[EPL];
+                int bs[EPL], len[EPL], rank[EPL];
+                int maxlen = 0;
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) {
+                    const int i = tid + q * NT;
+                    ki[q] = i < n ? sl.K[1][i] : 0u;
+                }
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) {
+                    const int i = tid + q * NT;
+                    const int d = ki[q] & (FL::ND - 1);
+                    bs[q] = i < n ? (int)sl.bstart[d] : 0;
+                    len[q] = i < n ? (int)sl.bstart[d + 1] - bs[q] : 0;
+                    rank[q] = 0;
+                    maxlen = max(maxlen, len[q]);
+                }
+                for (int j = 0; j < maxlen; ++j) {
+#pragma unroll
+                    for (int q = 0; q < EPL; ++q)
+                        if (j < len[q]) {
+                            const uint32_t kj = sl.K[1][bs[q] + j];
+                            rank[q] += (kj < ki[q] || (kj == ki[q] && bs[q] + j < (int)(tid + q * NT))) ? 1 : 0;
+                        }
+                }
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) {
+                    const int i = tid + q * NT;
+                    if (i < n) {
+                        sl.K[0][bs[q] + rank[q]] = ki[q];
+                        sl.V[0][bs[q] + rank[q]] = sl.V[1][i];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < EPL; ++q) {
+                    const int i = tid + q * NT;
+                    if (i >= n) continue;
+                    const uint32_t ki = sl.K[1][i];
+                    const int d = ki & (FL::ND - 1);
+                    const int bs = sl.bstart[d], be = sl.bstart[d + 1];
+                    int rank = 0;
+                    int j = bs;
+                    for (; j + 4 <= be; j += 4) {
+                        const uint32_t k0 = sl.K[1][j], k1 = sl.K[1][j + 1], k2 = sl.K[1][j + 2], k3 = sl.K[1][j + 3];
+                        rank += (k0 < ki || (k0 == ki && j < i)) + (k1 < ki || (k1 == ki && j + 1 < i)) +
+                                (k2 < ki || (k2 == ki && j + 2 < i)) + (k3 < ki || (k3 == ki && j + 3 < i));
+                    }
+                    for (; j < be; ++j) {
+                        const uint32_t kj = sl.K[1][j];
+                        rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+                    }
+                    sl.K[0][bs + rank] = ki;
+                    sl.V[0][bs + rank] = sl.V[1][i];
+                }
+            }
+            __syncthreads();
+            cur = 0;
+        } else {
+            for (int shift = FL::DB; shift < nbits; shift += FL::DB) {
+                fast_pass<NT, EPL, false>(n, shift, key, ok, sl.K[cur], sl.V[cur], sl.K[cur ^ 1], sl.V[cur ^ 1], sl, false);
+                cur ^= 1;
+            }
+        }
+    }
+    PHASE(10);
+    // ---- segments: thread tid owns sorted entries [EPL*tid, EPL*tid + EPL)
+    const uint32_t* K = sl.K[cur];
+    const int32_t* Vs = sl.V[cur];
+    int32_t* sseg = sl.V[cur ^ 1];
+    uint32_t* srow = sl.K[cur ^ 1];
+    const int64_t off = (int64_t)t * ix.cap;
+    int32_t* perm = ix.perm + off;
+    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int i = tid + q * NT;
+        if (i < n) perm[i] = Vs[i];
+    }
+    int h = 0;
+    bool head[EPL];
+    uint32_t kq[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int i = EPL * tid + q;
+        kq[q] = i < n ? K[i] : 0u;
+        const uint32_t kp = (i > 0 && i < n) ? K[i - 1] : ~kq[q];
+        head[q] = i < n && kp != kq[q];
+        h += head[q] ? 1 : 0;
+    }
+    int U;
+    int s = block_scan_nw<NT / 64, int>(h, sl.wtot, &U);
+#pragma unroll
+    for (int q = 0; q < EPL; ++q)
+        if (head[q]) {
+            const int i = EPL * tid + q;
+            sseg[s] = i;
+            srow[s] = kq[q];
+            seg_start[s] = i;
+            seg_row[s] = kq[q];
+            ++s;
+        }
+    if (tid == 0) seg_start[U] = n;
+    __syncthreads();
+    PHASE(20);
+    // packed counts (N <= 4096 < 2^21): chunks bits 0-20, hot segments 21-41, hot slices 42-62
+    constexpr long long M21 = (1ll << 21) - 1;
+    long long cw = 0;
+    int beg[EPL], end[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int sidx = EPL * tid + q;
+        beg[q] = end[q] = 0;
+        if (sidx < U) {
+            beg[q] = sseg[sidx];
+            end[q] = sidx + 1 < U ? sseg[sidx + 1] : n;
+            const int len = end[q] - beg[q];
+            cw += len <= kChunk ? 1ll : ((1ll << 21) | ((long long)((len + kHotSlice - 1) / kHotSlice) << 42));
+        }
+    }
+    long long tot64;
+    const long long ex = block_scan_nw<NT / 64, long long>(cw, sl.wtot64, &tot64);
+    int c = (int)(ex & M21), hh = (int)((ex >> 21) & M21), ss = (int)((ex >> 42) & M21);
+    int4* chunks = ix.chunks + off;
+    int4* hot = ix.hot + off;
+    int32_t* hot_slice = ix.hot_slice + off;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const int sidx = EPL * tid + q;
+        if (sidx < U) {
+            const int len = end[q] - beg[q];
+            if (len <= kChunk) {
+                chunks[c++] = make_int4(beg[q], end[q], (int)srow[sidx], Vs[beg[q]]);
+            } else {
+                const int ns = (len + kHotSlice - 1) / kHotSlice;
+                hot[hh] = make_int4(beg[q], end[q], (int)srow[sidx], ss);
+                for (int k = 0; k < ns; ++k) hot_slice[ss + k] = hh;
+                ++hh;
+                ss += ns;
+            }
+        }
+    }
+    if (tid == 0) {
+        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        cnt[CNT_U] = U; cnt[CNT_C] = (int)(tot64 & M21); cnt[CNT_H] = (int)((tot64 >> 21) & M21);
+        cnt[CNT_S] = (int)((tot64 >> 42) & M21); cnt[CNT_NV] = n;
+    }
+    PHASE(22);
+}
+
+}  // namespace dlrm

@@ -24,6 +24,7 @@
 // The interaction's arithmetic intensity (~11-24 flop/B) is far below the MFMA ridge, so
 // these kernels are HBM-bound; MFMA just keeps the VALU free and the operand traffic low.
 #include "common.hpp"
+#include "indexer.hpp"
 
 namespace dlrm {
 
@@ -255,21 +256,20 @@ __device__ __forceinline__ f32x4_t load4_f32(const uint16_t* p) {
 // GATHER: T_b is not read from a materialized ys but rebuilt from x (row 0) and the table
 // rows of the sample's one-hot indices (rows 1..F-1): the same values, without ys.
 template <typename T, int NB, bool GATHER>
-__global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
-                                                           int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
-                                                           float* __restrict__ dx, int64_t dx_ld,
-                                                           float* __restrict__ dt, int64_t dt_ld, GatherArgs ga,
-                                                           const T* __restrict__ x, int64_t x_ld) {
+__device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int d, int F, int B,
+                                         const T* __restrict__ dout, int64_t dout_ld, const T* __restrict__ t,
+                                         int64_t t_ld, float* __restrict__ dx, int64_t dx_ld,
+                                         float* __restrict__ dt, int64_t dt_ld, const GatherArgs& ga,
+                                         const T* __restrict__ x, int64_t x_ld) {
     typedef BwdGeom<NB> G;
     constexpr int KS = 4 * NB;  // max k-steps (F <= 16 NB)
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (w >= G::WPB) return;
     const int c = lane & 15, q = lane >> 4;
     float* S = smem + w * G::LDS_FLOATS;
     const int P = F * (F - 1) / 2;
     const int ksteps = (F + 3) / 4;
-    for (int64_t b = (int64_t)blockIdx.x * G::WPB + w; b < B; b += (int64_t)gridDim.x * G::WPB) {
+    for (int64_t b = (int64_t)bid * G::WPB + w; b < B; b += (int64_t)nblocks * G::WPB) {
         const T* ob = dout + b * dout_ld;
         const T* tb = GATHER ? nullptr : t + b * t_ld;
         const T* rowp[KS];  // GATHER: this lane's T rows kk = 4s + q
@@ -350,6 +350,41 @@ __global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, 
         }
         wave_lds_sync();
     }
+}
+
+template <typename T, int NB, bool GATHER>
+__global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
+                                                           int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
+                                                           float* __restrict__ dx, int64_t dx_ld,
+                                                           float* __restrict__ dt, int64_t dt_ld, GatherArgs ga,
+                                                           const T* __restrict__ x, int64_t x_ld) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    bwd_body<T, NB, GATHER>(blockIdx.x, gridDim.x, smem, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, ga,
+                            x, x_ld);
+}
+
+// The backward of a training step with the SparseIndexer build in the same grid: workgroups
+// [0, T) each sort one table's positions (indexer.hpp, 256 threads, while the backward's
+// workgroups stream), the rest run the re-gathering backward.  Occupancy 3 per SIMD leaves
+// room for the indexer's workgroups beside the backward's two per CU.
+constexpr int kBwdIndexEPL = 8;  // positions per thread: N <= 2048
+template <typename T, int NB>
+__global__ __launch_bounds__(256, 3) void interact_bwd_index_kernel(int d, int F, int B, const T* __restrict__ dout,
+                                                                    int64_t dout_ld, float* __restrict__ dx,
+                                                                    int64_t dx_ld, float* __restrict__ dt,
+                                                                    int64_t dt_ld, GatherArgs ga,
+                                                                    const T* __restrict__ x, int64_t x_ld,
+                                                                    IndexerDev ix) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int T_ = F - 1;
+    if ((int)blockIdx.x < T_) {
+        FastLds<256, kBwdIndexEPL>& sl = *(FastLds<256, kBwdIndexEPL>*)smem;
+        fast_index_table<256, kBwdIndexEPL>(ix, blockIdx.x, (uint32_t)ga.tabs[blockIdx.x].nrows, ga.idx, ga.itype,
+                                            ga.tstride, ga.base, B * ga.L, ga.err, sl);
+        return;
+    }
+    bwd_body<T, NB, true>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
+                          dt_ld, ga, x, x_ld);
 }
 
 // ------------------------------------------------------------------ scalar fallbacks
@@ -567,8 +602,39 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
-                               int64_t dx_ld, float* dt, int64_t dt_ld) {
+                               int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix) {
     GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
+    const int F = T_ + 1;
+    const int NB = (F + 15) / 16;
+    const int esz = dtype == DLRM_F32 ? 4 : 2;
+    if (ix && B > 0 && T_ > 0) {
+        const bool aligned = d % 4 == 0 && tabs_aligned16 && (uintptr_t)x % (4 * esz) == 0 && (x_ld % 4) == 0 &&
+                             (uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 && (dt_ld % 4) == 0;
+        if (aligned && NB <= 2 && (int64_t)B * L <= 256 * kBwdIndexEPL) {
+            hipStream_t s = ctx_stream(ctx);
+            const int cus = ctx_num_cus(ctx);
+            size_t lds = sizeof(FastLds<256, kBwdIndexEPL>);
+#define DLRM_LAUNCH_BWDIX(TY, N_)                                                                                 \
+    {                                                                                                              \
+        typedef BwdGeom<N_> G;                                                                                     \
+        const size_t blds = sizeof(float) * G::LDS_FLOATS * G::WPB;                                                \
+        if (blds > lds) lds = blds;                                                                                \
+        const unsigned g = grid_for(B, G::WPB, cus);                                                               \
+        hipLaunchKernelGGL((interact_bwd_index_kernel<TY, N_>), dim3(g + T_), dim3(256), lds, s, d, F, B,          \
+                           (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x, x_ld, *ix);           \
+    }
+            if (dtype == DLRM_F32) {
+                if (NB == 1) DLRM_LAUNCH_BWDIX(float, 1) else DLRM_LAUNCH_BWDIX(float, 2)
+            } else {
+                if (NB == 1) DLRM_LAUNCH_BWDIX(uint16_t, 1) else DLRM_LAUNCH_BWDIX(uint16_t, 2)
+            }
+#undef DLRM_LAUNCH_BWDIX
+            return ctx_hip(ctx, hipGetLastError(), "interact_bwd(+indexer) launch");
+        }
+        // no fused form for this shape: the indexer's own launch, then the backward
+        const int rc = launch_indexer_build(ctx, *ix, tabs, T_, idx, itype, tstride, base, B, L);
+        if (rc) return rc;
+    }
     return run_interact_bwd<true>(ctx, dtype, d, T_ + 1, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt, dt_ld, ga,
                                   tabs_aligned16, x, x_ld);
 }

@@ -25,22 +25,6 @@
 // rounding order).
 #include "common.hpp"
 
-namespace dlrm {
-
-constexpr int kBuildThreads = 1024;
-constexpr int kBuildWaves = kBuildThreads / 64;
-constexpr int kChunk = 32;          // max positions of a segment handled by one lane group
-constexpr int kLdsSortMax = 2048;   // positions per table sorted entirely in LDS
-constexpr int kDigits = 257;        // 256 row digits + 1 bucket that keeps invalid indices last
-constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
-
-enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
-
-// Hot segments are cut into slices of kHotSlice positions, one work item each; a segment of
-// several slices is combined by its last-arriving slice (sc1 partial rows + a counter).
-constexpr int kHotSlice = 128;
-int64_t indexer_slice_cap(int64_t cap) { return cap / kHotSlice + cap / (kChunk + 1) + 1; }
-
 #ifdef DLRM_PHASE
 // Phase timestamps (wall_clock64, 100 MHz) of one indexer block + start/end of every block;
 // built only into the profiling variant of the library (tools/phase_indexer.py).
@@ -70,33 +54,19 @@ extern "C" int dlrm_debug_apply_reset(void) {
 #define APPLY_END() do {} while (0)
 #endif
 
-// Exclusive scan over the 1024 threads of the block; returns this thread's prefix, total in *tot.
+#include "indexer.hpp"
+
+namespace dlrm {
+
+constexpr int kBuildThreads = 1024;
+constexpr int kBuildWaves = kBuildThreads / 64;
+constexpr int kLdsSortMax = 2048;   // positions per table sorted entirely in LDS
+constexpr int kDigits = 257;        // 256 row digits + 1 bucket that keeps invalid indices last
+
+int64_t indexer_slice_cap(int64_t cap) { return cap / kHotSlice + cap / (kChunk + 1) + 1; }
+
 template <typename V>
-__device__ __forceinline__ V block_scan_excl(V v, V* wtot, V* tot) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    V x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const V y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63) wtot[w] = x;
-    __syncthreads();
-    if (w == 0) {
-        V t = lane < kBuildWaves ? wtot[lane] : V(0);
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const V y = __shfl_up(t, off, 64);
-            if (lane >= off) t += y;
-        }
-        if (lane < kBuildWaves) wtot[kBuildWaves + lane] = t;  // inclusive wave totals
-    }
-    __syncthreads();
-    const V before = w ? wtot[kBuildWaves + w - 1] : V(0);
-    *tot = wtot[2 * kBuildWaves - 1];
-    __syncthreads();  // wtot reusable after return
-    return before + x - v;
-}
+__device__ __forceinline__ V block_scan_excl(V v, V* wtot, V* tot) { return block_scan_nw<kBuildWaves, V>(v, wtot, tot); }
 
 struct SortLds {
     int cnt[kBuildWaves][kDigits + 7];  // per-wave digit counts, then their global offsets
@@ -335,276 +305,18 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
 #endif
 }
 
-// ------------------------------------------------------------------- fast indexer (N <= 4096)
-// One 1024-thread workgroup per table; everything stays in LDS.
-//  * Stable counting pass on an 8-bit digit: wave w walks positions [w*S, (w+1)*S) (S = 64*EPL)
-//    in tiles of 64, so "earlier position" = earlier wave, earlier tile or lower lane.  Lanes
-//    sharing a digit are found with 8 ballots; each wave keeps its running count of every
-//    digit in its own column of cnt[digit][wave] (only that wave touches it, in program
-//    order), which gives each key its rank among the wave's earlier equal digits.  One block
-//    scan over cnt in (digit, wave) order turns the counts into output offsets: no serial
-//    cross-wave loop.  Invalid indices are dropped (they raised the bounds flag).
-//  * Rows of <= 8 bits are then grouped.  Larger rows: when every bucket is small (uniform
-//    rows: N/256 keys per bucket) each bucket is ordered by a direct rank on (row, position);
-//    skewed rows take the remaining LSD passes.
-//  * Segments and the chunk / hot lists: one head-flag scan and one packed 64-bit scan.
-// Output format = indexer_build_kernel's (the apply kernel and dlrm_indexer_read unchanged).
-constexpr int kFastThreads = 1024;
-constexpr int kFastWaves = kFastThreads / 64;
-constexpr int kFastBits = 8;
-constexpr int kFastDigits = 1 << kFastBits;
-constexpr int kFastMaxN = 4096;
-static_assert(kFastDigits * kFastWaves == 4 * kFastThreads, "4 (digit, wave) counters per thread");
-
-template <int EPL>
-struct FastLds {
-    uint16_t cnt[kFastDigits][kFastWaves];  // digit-major: per-wave counts, then output offsets
-    uint16_t bstart[kFastDigits + 8];       // first-pass bucket starts
-    uint32_t K[2][kFastThreads * EPL];
-    int32_t V[2][kFastThreads * EPL];
-    int wtot[2 * kFastWaves];
-    long long wtot64[2 * kFastWaves];
-    int maxbucket;
-};
-
-// One stable counting pass.  FROM_REGS: the first pass's keys come from registers (tile j
-// of wave w = position w*S + 64j + lane); otherwise from kin/vin[0, n) in LDS.  Returns the
-// number of keys written to kout/vout.
-template <int EPL, bool FROM_REGS>
-__device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bool (&rok)[EPL],
-                         const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
-                         FastLds<EPL>& sl, bool first) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    constexpr int S = 64 * EPL;
-    ((uint2*)&sl.cnt[0][0])[tid] = make_uint2(0, 0);  // 4 counters per thread
-    uint32_t key[EPL];
-    int32_t val[EPL];
-    bool ok[EPL];
-    int lr[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) {
-        const int i = w * S + j * 64 + lane;
-        if (FROM_REGS) {
-            key[j] = rkey[j];
-            ok[j] = rok[j];
-            val[j] = i;
-        } else {
-            ok[j] = i < n;
-            key[j] = ok[j] ? kin[i] : 0u;
-            val[j] = ok[j] ? vin[i] : 0;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) {
-        const uint32_t d = (key[j] >> shift) & (kFastDigits - 1);
-        unsigned long long peers = __ballot(ok[j]);
-#pragma unroll
-        for (int bit = 0; bit < kFastBits; ++bit) {
-            const unsigned long long bb = __ballot(ok[j] && ((d >> bit) & 1u));
-            peers &= ((d >> bit) & 1u) ? bb : ~bb;
-        }
-        int base = 0;
-        if (ok[j] && j > 0) base = sl.cnt[d][w];
-        lr[j] = base + __popcll(peers & lt);
-        if (ok[j] && (peers & lt) == 0) sl.cnt[d][w] = (uint16_t)(base + __popcll(peers));
-    }
-    __syncthreads();
-    // (digit, wave) offsets: thread tid owns counters [4 tid, 4 tid + 4) = digit tid/4, waves 4(tid%4)..
-    const uint2 raw = ((const uint2*)&sl.cnt[0][0])[tid];
-    const int c0 = raw.x & 0xffff, c1 = raw.x >> 16, c2 = raw.y & 0xffff, c3 = raw.y >> 16;
-    int total;
-    const int ex = block_scan_excl<int>(c0 + c1 + c2 + c3, sl.wtot, &total);
-    ((uint2*)&sl.cnt[0][0])[tid] =
-        make_uint2((uint32_t)ex | ((uint32_t)(ex + c0) << 16), (uint32_t)(ex + c0 + c1) | ((uint32_t)(ex + c0 + c1 + c2) << 16));
-    if (first) {
-        if ((tid & 3) == 0) sl.bstart[tid >> 2] = (uint16_t)ex;
-        if (tid == 0) {
-            sl.bstart[kFastDigits] = (uint16_t)total;
-            sl.maxbucket = 0;
-        }
-    }
-    __syncthreads();
-    if (first) {
-        // largest bucket (decides rank sort vs more passes): digit d's size = bstart[d+1] - bstart[d]
-        int m = tid < kFastDigits ? (int)sl.bstart[tid + 1] - (int)sl.bstart[tid] : 0;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-        if (lane == 0 && m > 0) atomicMax(&sl.maxbucket, m);
-    }
-#pragma unroll
-    for (int j = 0; j < EPL; ++j)
-        if (ok[j]) {
-            const uint32_t d = (key[j] >> shift) & (kFastDigits - 1);
-            const int dst = sl.cnt[d][w] + lr[j];
-            kout[dst] = key[j];
-            vout[dst] = val[j];
-        }
-    __syncthreads();
-    return total;
-}
-
-template <int EPL>
-__device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, const void* __restrict__ idx,
-                                 int itype, int64_t tstride, int base, int N, unsigned* __restrict__ err,
-                                 FastLds<EPL>& sl) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr int S = 64 * EPL;
-    const int nbits = 32 - __clz(nrows > 0 ? nrows - 1 : 0);
-    // the indices, read once (coalesced 64-lane runs, all loads in flight) and validated
-    uint32_t key[EPL];
-    bool ok[EPL];
-    int64_t raw[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) {
-        const int i = w * S + j * 64 + lane;
-        raw[j] = load_index(idx, itype, t * tstride + min(i, N - 1));
-    }
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) {
-        const int i = w * S + j * 64 + lane;
-        const int64_t r = raw[j] - base;
-        ok[j] = i < N && r >= 0 && r < (int64_t)nrows;
-        key[j] = ok[j] ? (uint32_t)r : 0u;
-        if (i < N && !ok[j]) raise_index_error(err);
-    }
-    PHASE(1);
-    const int n = fast_pass<EPL, true>(N, 0, key, ok, nullptr, nullptr, sl.K[1], sl.V[1], sl, true);
-    PHASE(5);
-    int cur = 1;
-    if (nbits > kFastBits) {
-        if (sl.maxbucket <= kRankBucketMax) {
-            // order each bucket by (row, position); the stable pass kept positions ascending
-#pragma unroll
-            for (int q = 0; q < EPL; ++q) {
-                const int i = tid + q * kFastThreads;
-                if (i >= n) continue;
-                const uint32_t ki = sl.K[1][i];
-                const int d = ki & (kFastDigits - 1);
-                const int bs = sl.bstart[d], be = sl.bstart[d + 1];
-                int rank = 0;
-                int j = bs;
-                for (; j + 4 <= be; j += 4) {
-                    const uint32_t k0 = sl.K[1][j], k1 = sl.K[1][j + 1], k2 = sl.K[1][j + 2], k3 = sl.K[1][j + 3];
-                    rank += (k0 < ki || (k0 == ki && j < i)) + (k1 < ki || (k1 == ki && j + 1 < i)) +
-                            (k2 < ki || (k2 == ki && j + 2 < i)) + (k3 < ki || (k3 == ki && j + 3 < i));
-                }
-                for (; j < be; ++j) {
-                    const uint32_t kj = sl.K[1][j];
-                    rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
-                }
-                sl.K[0][bs + rank] = ki;
-                sl.V[0][bs + rank] = sl.V[1][i];
-            }
-            __syncthreads();
-            cur = 0;
-        } else {
-            for (int shift = kFastBits; shift < nbits; shift += kFastBits) {
-                fast_pass<EPL, false>(n, shift, key, ok, sl.K[cur], sl.V[cur], sl.K[cur ^ 1], sl.V[cur ^ 1], sl, false);
-                cur ^= 1;
-            }
-        }
-    }
-    PHASE(10);
-    // ---- segments: thread tid owns sorted entries [EPL*tid, EPL*tid + EPL)
-    const uint32_t* K = sl.K[cur];
-    const int32_t* Vs = sl.V[cur];
-    int32_t* sseg = sl.V[cur ^ 1];
-    uint32_t* srow = sl.K[cur ^ 1];
-    const int64_t off = (int64_t)t * ix.cap;
-    int32_t* perm = ix.perm + off;
-    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
-    uint32_t* seg_row = ix.seg_row + off;
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const int i = tid + q * kFastThreads;
-        if (i < n) perm[i] = Vs[i];
-    }
-    int h = 0;
-    bool head[EPL];
-    uint32_t kq[EPL];
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const int i = EPL * tid + q;
-        kq[q] = i < n ? K[i] : 0u;
-        const uint32_t kp = (i > 0 && i < n) ? K[i - 1] : ~kq[q];
-        head[q] = i < n && kp != kq[q];
-        h += head[q] ? 1 : 0;
-    }
-    int U;
-    int s = block_scan_excl<int>(h, sl.wtot, &U);
-#pragma unroll
-    for (int q = 0; q < EPL; ++q)
-        if (head[q]) {
-            const int i = EPL * tid + q;
-            sseg[s] = i;
-            srow[s] = kq[q];
-            seg_start[s] = i;
-            seg_row[s] = kq[q];
-            ++s;
-        }
-    if (tid == 0) seg_start[U] = n;
-    __syncthreads();
-    PHASE(20);
-    // packed counts (N <= 4096 < 2^21): chunks bits 0-20, hot segments 21-41, hot slices 42-62
-    constexpr long long M21 = (1ll << 21) - 1;
-    long long cw = 0;
-    int beg[EPL], end[EPL];
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const int sidx = EPL * tid + q;
-        beg[q] = end[q] = 0;
-        if (sidx < U) {
-            beg[q] = sseg[sidx];
-            end[q] = sidx + 1 < U ? sseg[sidx + 1] : n;
-            const int len = end[q] - beg[q];
-            cw += len <= kChunk ? 1ll : ((1ll << 21) | ((long long)((len + kHotSlice - 1) / kHotSlice) << 42));
-        }
-    }
-    long long tot64;
-    const long long ex = block_scan_excl<long long>(cw, sl.wtot64, &tot64);
-    int c = (int)(ex & M21), hh = (int)((ex >> 21) & M21), ss = (int)((ex >> 42) & M21);
-    int4* chunks = ix.chunks + off;
-    int4* hot = ix.hot + off;
-    int32_t* hot_slice = ix.hot_slice + off;
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const int sidx = EPL * tid + q;
-        if (sidx < U) {
-            const int len = end[q] - beg[q];
-            if (len <= kChunk) {
-                chunks[c++] = make_int4(beg[q], end[q], (int)srow[sidx], Vs[beg[q]]);
-            } else {
-                const int ns = (len + kHotSlice - 1) / kHotSlice;
-                hot[hh] = make_int4(beg[q], end[q], (int)srow[sidx], ss);
-                for (int k = 0; k < ns; ++k) hot_slice[ss + k] = hh;
-                ++hh;
-                ss += ns;
-            }
-        }
-    }
-    if (tid == 0) {
-        int32_t* cnt = ix.counts + (int64_t)t * 8;
-        cnt[CNT_U] = U; cnt[CNT_C] = (int)(tot64 & M21); cnt[CNT_H] = (int)((tot64 >> 21) & M21);
-        cnt[CNT_S] = (int)((tot64 >> 42) & M21); cnt[CNT_NV] = n;
-    }
-    PHASE(22);
-}
-
-template <int EPL>
-__global__ __launch_bounds__(kFastThreads) void indexer_fast_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
-                                                                    const void* __restrict__ idx, int itype,
-                                                                    int64_t tstride, int base, int N,
-                                                                    unsigned* __restrict__ err) {
+template <int NT, int EPL>
+__global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
+                                                          const void* __restrict__ idx, int itype, int64_t tstride,
+                                                          int base, int N, unsigned* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    FastLds<EPL>& sl = *(FastLds<EPL>*)dyn;
+    FastLds<NT, EPL>& sl = *(FastLds<NT, EPL>*)dyn;
     const int t = blockIdx.x;
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
 #endif
     PHASE(0);
-    fast_index_table<EPL>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
+    fast_index_table<NT, EPL>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
 #endif
@@ -1009,15 +721,22 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-    if (N <= kFastThreads * 2) {
-        hipLaunchKernelGGL(indexer_fast_kernel<2>, dim3(T_), dim3(kFastThreads), sizeof(FastLds<2>), s, ix, tabs, idx,
-                           itype, tstride, base, (int)N, ctx_error_word(ctx));
+#ifdef DLRM_PHASE
+    if (getenv("DLRM_IX256") && N <= 2048) {  // profiling: the 256-thread form the backward launch uses
+        hipLaunchKernelGGL((indexer_fast_kernel<256, 8>), dim3(T_), dim3(256), sizeof(FastLds<256, 8>), s, ix, tabs,
+                           idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
+        return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
+    }
+#endif
+    if (N <= 1024 * 2) {
+        hipLaunchKernelGGL((indexer_fast_kernel<1024, 2>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 2>), s, ix, tabs,
+                           idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
     } else if (N <= kFastMaxN) {
-        static const hipError_t a4 = hipFuncSetAttribute((const void*)indexer_fast_kernel<4>,
+        static const hipError_t a4 = hipFuncSetAttribute((const void*)indexer_fast_kernel<1024, 4>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                         (int)sizeof(FastLds<4>));
+                                                         (int)sizeof(FastLds<1024, 4>));
         (void)a4;
-        hipLaunchKernelGGL(indexer_fast_kernel<4>, dim3(T_), dim3(kFastThreads), sizeof(FastLds<4>), s, ix, tabs, idx,
+        hipLaunchKernelGGL((indexer_fast_kernel<1024, 4>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 4>), s, ix, tabs, idx,
                            itype, tstride, base, (int)N, ctx_error_word(ctx));
     } else
         hipLaunchKernelGGL(indexer_build_kernel<false>, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, idx, itype,

@@ -94,9 +94,10 @@ class HotPath:
         self._check(self.lib.dlrm_indexer_build(h, self.indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
                                                 idx.stride, self.index_base, self.B, self.L))
 
-    def interact_bwd(self, dout, x=None, idx=None):
+    def interact_bwd(self, dout, x=None, idx=None, build_indexer=False):
         """dot_back.  Without a materialized ys, T is rebuilt from x and the indices of the
-        forward (the last forward's unless given)."""
+        forward (the last forward's unless given); build_indexer: the same launch also builds
+        the update's indexer from those indices."""
         h = self.ctx.bind()
         if self.materialize_ys:
             self._check(self.lib.dlrm_interact_bwd(h, self.dcode, self.d, self.F, self.B, ptr(dout), dout.stride(0),
@@ -107,7 +108,8 @@ class HotPath:
         idx = self._fwd_idx if idx is None else idx
         if x is None or idx is None:
             raise RuntimeError("interact_bwd without a materialized ys needs the forward's x and indices")
-        self._check(self.lib.dlrm_interact_bwd_gather(h, self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
+        ixh = self.indexer.handle if (build_indexer and self.indexer is not None) else None
+        self._check(self.lib.dlrm_interact_bwd_gather(h, self.ts.handle, ixh, ptr(idx.data), idx.itype, idx.stride,
                                                       self.index_base, self.B, self.L, ptr(x), x.stride(0),
                                                       ptr(dout), dout.stride(0), self.padding, ptr(self.dx),
                                                       self.dx.stride(0), ptr(self.dt), self.dt.stride(0)))
@@ -152,8 +154,10 @@ class HotPath:
         return self.out
 
     def backward(self, idx, dout):
-        self.interact_bwd(dout, idx=idx)
-        prebuilt = False
+        # without ys (and deterministic), the indexer is built inside the backward's launch
+        in_bwd = not self.materialize_ys and self.indexer is not None and not self.overlap_indexer
+        self.interact_bwd(dout, idx=idx, build_indexer=in_bwd)
+        prebuilt = in_bwd
         if self.overlap_indexer and self._indexer_done is not None:
             torch.cuda.current_stream(self.ts.device).wait_event(self._indexer_done)
             prebuilt = True

@@ -142,14 +142,13 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
 /* dot_back as dlrm_interact_bwd, with T_b rebuilt from x (row 0) and the tables' rows of the
  * sample's one-hot indices (rows 1..F-1) instead of read from a materialized ys: the same
  * values while the tables are unchanged since the forward (recomputation, not a cache).
- * lookups must be 1; dtype is the tables' (dout and x in it); dx, dt fp32 as above. */
-int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tables,
-                             const void* indices, int itype, int64_t table_stride, int index_base,
-                             int batch, int lookups, const void* x, int64_t x_ld,
-                             const void* dout, int64_t dout_ld, int padding,
-                             float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
+ * lookups must be 1; dtype is the tables' (dout and x in it); dx, dt fp32 as above.
+ * indexer (may be NULL): also builds it from the same indices, as dlrm_indexer_build would --
+ * in the same launch where the shape allows (its workgroups sort while the backward's stream),
+ * so the step's dlrm_sgd_update can pass DLRM_UPDATE_PREBUILT.
+ * Declared after the indexer type below; see the SparseIndexer section. */
 
-/* ---- sparse indexer + SGD scatter update --------------------------------------------- */
+/* ---- sparse indexer + SGD scatter update/* ---- sparse indexer + SGD scatter update --------------------------------------------- */
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_table,
                         dlrm_indexer** out);
 int dlrm_indexer_destroy(dlrm_indexer* indexer);
@@ -165,6 +164,13 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* 
 int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
                       int64_t* num_unique, int64_t* rows, int64_t* positions,
                       int64_t* seg_start, int64_t cap);
+
+/* Backward of a training step without a materialized ys (see above). */
+int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tables, dlrm_indexer* indexer,
+                             const void* indices, int itype, int64_t table_stride, int index_base,
+                             int batch, int lookups, const void* x, int64_t x_ld,
+                             const void* dout, int64_t dout_ld, int padding,
+                             float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 
 /* update!(Descent(lr), tables, grads, indexers):
  *   table_t[r] -= lr * sum_{(b,k): idx_t[b*lookups+k] - base == r} grad[b][grad_offset + t*dim + :]

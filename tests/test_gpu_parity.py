@@ -215,15 +215,47 @@ def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
     tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B * L, gpu)
     ix.build(tabs, torch.from_numpy(idx).reshape(len(rows), B, L).to(gpu), index_base=0)
-    for t in range(len(rows)):
+    _assert_segments(ix, idx, B * L)
+
+
+def _assert_segments(ix, idx, N):
+    for t in range(idx.shape[0]):
         urows, _ = _np_segments(idx[t])
         got_rows, pos, seg = ix.segments(t)
         assert sorted(got_rows) == urows.tolist()  # one segment per distinct row (segment order unspecified)
-        assert seg[-1] == B * L and len(seg) == len(urows) + 1
+        assert seg[-1] == N and len(seg) == len(urows) + 1
         for s_, r in enumerate(got_rows):
             members = pos[seg[s_]:seg[s_ + 1]]
             want = np.flatnonzero(idx[t] == r).tolist()
             assert members == want  # exactly this row's positions, ascending
+
+
+@pytest.mark.parametrize("rows,B,zipf", [([3, 4, 10, 1000, 5_000_000], 2048, None), ([300, 100000, 5_000_000], 2048, 1.1),
+                                         ([256, 257, 70000], 2048, None), ([0x10000, 0x1000000], 1500, None),
+                                         ([2], 1, None), ("kaggle", 2048, None), ([100000, 3], 5000, None),
+                                         ([50] * 40, 512, None)])
+def test_backward_built_indexer(pkg, gpu, rows, B, zipf):
+    """dlrm_interact_bwd_gather with an indexer: the indexer built in the backward's launch
+    (256-thread workgroups beside the backward's; or its own launch where the shape has no
+    fused form: N > 2048, F > 32) groups positions exactly, and the backward is unchanged."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    rng = np.random.default_rng(B + len(rows))
+    D = 16
+    idx = rand_indices(rng, rows, B, 1, zipf=zipf)
+    tabs = pkg.EmbeddingTableSet([torch.randn((n, D), device=gpu) for n in rows])
+    hp = pkg.HotPath(tabs, B, 1, index_base=0)
+    assert not hp.materialize_ys
+    p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(len(rows), B, 1).to(gpu))
+    x = torch.randn((B, D), device=gpu)
+    dout = torch.randn((B, hp.width), device=gpu)
+    hp.interact_bwd(dout, x=x, idx=p)
+    dx0, dt0 = hp.dx.clone(), hp.dt.clone()
+    hp.interact_bwd(dout, x=x, idx=p, build_indexer=True)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    assert torch.equal(hp.dx, dx0) and torch.equal(hp.dt, dt0)
+    _assert_segments(hp.indexer, idx, B)
 
 
 @pytest.mark.parametrize("dim", [16, 128, 256, 8, 12])
