@@ -68,6 +68,36 @@ def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks, materialize_ys=True):
     }
 
 
+def step_api_bytes(B, T, D, L, E, I, st):
+    """Per-launch algorithmic HBM bytes of the training-step pair (dlrm_step_fwd / dlrm_step_bwd),
+    from the batch's index statistics st: n1 = positions whose row is hit once (updated inside the
+    backward), n2 = the other positions, u2 = their distinct rows (one apply chunk each)."""
+    d, F = D, T + 1
+    P = F * (F - 1) // 2
+    N = B * L
+    gather = B * (d * E + T * L * (I + D * E))          # x + the indices + the gathered rows
+    indexer = T * N * I + T * N * 4 + st["uniq"] * 8 + st["u2"] * 16 + T * N  # + perm, segments, chunks, flags
+    return {
+        "lookup_interact_fwd": gather + B * (d + P) * E + indexer,
+        # dout, x, the re-gathered rows, the once-hit flags; dx and dt's x rows, dt rows of repeated
+        # positions, once-hit rows written back after their SGD step
+        "interact_bwd": B * (d + P) * E + gather + T * N + B * (d * 4 + D * 4) + st["n2"] * D * 4 + st["n1"] * D * E,
+        "sgd_update": st["n2"] * (4 + D * 4) + st["u2"] * (2 * D * E + 16),
+    }
+
+
+def index_stats(idx_np):
+    """idx_np: [T][N] -> n1 (positions of once-hit rows), n2 (the rest), u2 (distinct repeated rows), uniq."""
+    n1 = n2 = u2 = uniq = 0
+    for row in idx_np:
+        _, cnt = np.unique(row, return_counts=True)
+        uniq += len(cnt)
+        n1 += int((cnt == 1).sum())
+        n2 += int(cnt[cnt > 1].sum())
+        u2 += int((cnt > 1).sum())
+    return {"n1": n1, "n2": n2, "u2": u2, "uniq": uniq}
+
+
 def make_inputs(pkg, w, B, dev, rank, T_rows):
     """Tables ~ ScaledUniform (model.jl:61-65), x ~ N(0,1), dout ~ N(0, 1e-3)."""
     g = torch.Generator(device=dev).manual_seed(51234 + rank)  # model.jl:193 seed
@@ -278,13 +308,30 @@ def main():
 
         in_bwd = (engine.fused and not engine.materialize_ys and engine.indexer is not None
                   and not engine.overlap_indexer)
+        if engine.step_api:
+            sts = [index_stats(packs[k].data.reshape(T, B * L).cpu().numpy()) for k in range(NBATCH)]
+            st = {key: sum(v[key] for v in sts) / NBATCH for key in sts[0]}
+            bytes_ = step_api_bytes(B, T, D, L, E, 4, st)
+            for k in range(NBATCH):  # batch k's split indexer, built by its own step forward
+                engine.indexer = indexers[k]
+                engine.step_fwd(x, packs[k])
+            engine.indexer = home
+
+            def sbwd_k(k, flags):
+                engine.indexer = indexers[k]
+                engine.step_bwd(dout, x=x, idx=packs[k], flags=flags)
+                engine.indexer = home
 
         def bwd_index_k(k):
             engine.indexer = indexers[k]
             engine.interact_bwd(dout, x=x, idx=packs[k], build_indexer=True)
             engine.indexer = home
 
-        if in_bwd:  # the indexer is built inside the backward's launch
+        if engine.step_api:  # indexer in the forward's launch; once-hit rows updated by the backward
+            names = ["lookup_interact_fwd", "interact_bwd", "sgd_update"]
+            fns = [lambda k: engine.step_fwd(x, packs[k]), lambda k: sbwd_k(k, pkg._lib.STEP_BWD_ONLY),
+                   lambda k: sbwd_k(k, pkg._lib.STEP_APPLY_ONLY)]
+        elif in_bwd:  # the indexer is built inside the backward's launch
             names = ["lookup_interact_fwd", "interact_bwd", "sgd_update"]
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), bwd_index_k, apply_k]
             bytes_["interact_bwd"] += bytes_["indexer_build"]
@@ -359,7 +406,9 @@ def main():
                        "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + RCCL all-to-all",
                        "launch": f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else "eager",
                        "ys": ("materialized" if world > 1 or engine.materialize_ys
-                              else "not materialized (backward re-gathers T)")},
+                              else "not materialized (backward re-gathers T)"),
+                       "step": ("dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "
+                                "updated in the backward)" if world == 1 and engine.step_api else "operators")},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -20,6 +20,7 @@ OK, E_ARG, E_HIP, E_INDEX, E_UNSUPPORTED, E_NOMEM, E_STATE = 0, -1, -2, -3, -4, 
 F32, BF16 = 0, 1
 I32, I64 = 0, 1
 UPDATE_ATOMIC, UPDATE_PREBUILT = 1, 2
+STEP_BWD_ONLY, STEP_APPLY_ONLY = 1, 2
 
 
 class DLRMError(RuntimeError):
@@ -68,6 +69,9 @@ SIGNATURES = {
     "dlrm_indexer_build": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32]),
     "dlrm_indexer_read": (_i32, [_vp, _vp, _i32, _pi64, _pi64, _pi64, _pi64, _i64]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
+    "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
+    "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
+                             _i64, _f32, _u32]),
 }
 
 _lib = None

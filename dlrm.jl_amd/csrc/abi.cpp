@@ -39,6 +39,7 @@ struct dlrm_indexer {
     void* partial_big = nullptr;  // partial rows for D > kPartialDim (allocated on first use)
     // recorded by the last build
     bool built = false;
+    bool split = false;  // built by dlrm_step_fwd's kernel: once-hit rows are left to the backward
     const void* indices = nullptr;
     int itype = 0, base = 0, B = 0, L = 0;
     int64_t tstride = 0;
@@ -69,6 +70,24 @@ int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what) {
     } while (0)
 
 static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice"); }
+
+static void record_build(dlrm_indexer* ix, bool split, const void* indices, int itype, int64_t tstride, int base,
+                         int B, int L) {
+    ix->built = true;
+    ix->split = split;
+    ix->indices = indices;
+    ix->itype = itype;
+    ix->tstride = tstride;
+    ix->base = base;
+    ix->B = B;
+    ix->L = L;
+}
+
+static bool built_from(const dlrm_indexer* ix, const void* indices, int itype, int64_t tstride, int base, int B,
+                       int L) {
+    return ix->built && ix->indices == indices && ix->B == B && ix->L == L && ix->itype == itype &&
+           ix->tstride == tstride && ix->base == base;
+}
 
 extern "C" {
 
@@ -303,13 +322,8 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer*
                                     index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld,
                                     ix ? &ix->dev : nullptr);
     if (rc || !ix) return rc;
-    ix->built = true;  // as dlrm_indexer_build: a following update may pass DLRM_UPDATE_PREBUILT
-    ix->indices = indices;
-    ix->itype = itype;
-    ix->tstride = table_stride;
-    ix->base = index_base;
-    ix->B = batch;
-    ix->L = lookups;
+    // as dlrm_indexer_build: a following update may pass DLRM_UPDATE_PREBUILT
+    record_build(ix, false, indices, itype, table_stride, index_base, batch, lookups);
     return DLRM_OK;
 }
 
@@ -337,7 +351,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot, n * 16},
         {(void**)&ix->dev.hot_slice, n * 4}, {(void**)&ix->dev.hot_cnt, n * 4},
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
-        {(void**)&ix->dev.counts, (size_t)T * 32},
+        {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n},
     };
     size_t total = 0;
     for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
@@ -376,13 +390,7 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
               (long long)batch * lookups, (long long)ix->dev.cap);
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups);
     if (rc) return rc;
-    ix->built = true;
-    ix->indices = indices;
-    ix->itype = itype;
-    ix->tstride = table_stride;
-    ix->base = index_base;
-    ix->B = batch;
-    ix->L = lookups;
+    record_build(ix, false, indices, itype, table_stride, index_base, batch, lookups);
     return DLRM_OK;
 }
 
@@ -420,6 +428,23 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t*
     return rc;
 }
 
+// multi-slice hot segments keep partial rows of D elements (allocated on first use for D > kPartialDim;
+// not on a launch path that is captured: the first update of a shape runs before capture)
+static int ensure_partials(dlrm_ctx* ctx, dlrm_indexer* ix, int D) {
+    if (D <= ix->dev.pdim) return DLRM_OK;
+    void* p = nullptr;
+    int rc = hip_set(ctx);
+    if (rc == DLRM_OK)
+        rc = ctx_hip(ctx, hipMalloc(&p, (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.pcap * D * 4),
+                     "hipMalloc(indexer partials)");
+    if (rc) return rc;
+    if (ix->partial_big) (void)hipFree(ix->partial_big);
+    ix->partial_big = p;
+    ix->dev.partial = (float*)p;
+    ix->dev.pdim = D;
+    return DLRM_OK;
+}
+
 int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned flags, const void* indices, int itype,
                     int64_t table_stride, int index_base, int batch, int lookups, const void* grad, int grad_dtype,
                     int64_t grad_ld, int64_t grad_offset, float lr) {
@@ -437,27 +462,84 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned f
     }
     CHECK_ARG(ix, "dlrm_sgd_update: deterministic mode needs an indexer");
     if (flags & DLRM_UPDATE_PREBUILT) {
-        if (!ix->built || ix->indices != indices || ix->B != batch || ix->L != lookups || ix->itype != itype ||
-            ix->tstride != table_stride || ix->base != index_base)
+        if (!built_from(ix, indices, itype, table_stride, index_base, batch, lookups))
             return ctx_fail(ctx, DLRM_E_STATE, "dlrm_sgd_update: indexer was not built from these indices");
+        if (ix->split)
+            return ctx_fail(ctx, DLRM_E_STATE,
+                            "dlrm_sgd_update: indexer was built by dlrm_step_fwd (once-hit rows are updated by "
+                            "dlrm_step_bwd); rebuild it or call dlrm_step_bwd");
     } else {
         rc = dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, lookups);
         if (rc) return rc;
     }
-    if (tb->D > ix->dev.pdim) {  // multi-slice hot segments keep partial rows of D elements
-        void* p = nullptr;
-        rc = hip_set(ctx);
-        if (rc == DLRM_OK)
-            rc = ctx_hip(ctx, hipMalloc(&p, (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.pcap * tb->D * 4),
-                         "hipMalloc(indexer partials)");
-        if (rc) return rc;
-        if (ix->partial_big) (void)hipFree(ix->partial_big);
-        ix->partial_big = p;
-        ix->dev.partial = (float*)p;
-        ix->dev.pdim = tb->D;
-    }
+    rc = ensure_partials(ctx, ix, tb->D);
+    if (rc) return rc;
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
                             (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr);
+}
+
+// ----------------------------------------------------------------------- training step
+int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
+                  int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld, void* out,
+                  int64_t out_ld, int padding) {
+    CHECK_ARG(ctx && tb && ix, "dlrm_step_fwd: null ctx/tables/indexer");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    CHECK_ARG(tb->T == ix->T, "dlrm_step_fwd: indexer has %d tables, tables has %d", ix->T, tb->T);
+    CHECK_ARG(batch <= ix->dev.cap, "dlrm_step_fwd: batch %d > indexer capacity %lld", batch, (long long)ix->dev.cap);
+    const int d = tb->D, F = tb->T + 1;
+    const int64_t P = (int64_t)F * (F - 1) / 2;
+    CHECK_ARG(padding >= 0 && x_ld >= d && out_ld >= d + P + padding, "dlrm_step_fwd: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (x && out), "dlrm_step_fwd: null buffer");
+    ix->built = false;
+    rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
+                         batch, x, x_ld, out, out_ld, padding, ix->dev);
+    if (rc == DLRM_OK) {
+        record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+        return DLRM_OK;
+    }
+    if (rc != DLRM_E_UNSUPPORTED) return rc;
+    // no single-launch form for this shape: the fused forward, then the (unsplit) indexer
+    rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                    index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding);
+    if (rc == DLRM_E_UNSUPPORTED)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
+                        "dlrm_step_fwd: no fused forward for this shape (16-B aligned rows and x, F <= 96 needed)");
+    if (rc) return rc;
+    return dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, 1);
+}
+
+int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
+                  int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld, const void* dout,
+                  int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr,
+                  unsigned flags) {
+    CHECK_ARG(ctx && tb && ix, "dlrm_step_bwd: null ctx/tables/indexer");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    const int d = tb->D, F = tb->T + 1;
+    const int64_t P = (int64_t)F * (F - 1) / 2;
+    CHECK_ARG(padding >= 0 && x_ld >= d && dout_ld >= d + P + padding && dx_ld >= d && dt_ld >= (int64_t)F * d,
+              "dlrm_step_bwd: leading dimensions too small");
+    CHECK_ARG(batch == 0 || (x && dout && dx && dt), "dlrm_step_bwd: null buffer");
+    if (!built_from(ix, indices, itype, table_stride, index_base, batch, 1))
+        return ctx_fail(ctx, DLRM_E_STATE, "dlrm_step_bwd: the indexer was not built by dlrm_step_fwd from these indices");
+    CHECK_ARG(flags != (DLRM_STEP_BWD_ONLY | DLRM_STEP_APPLY_ONLY), "dlrm_step_bwd: flags %u", flags);
+    rc = ensure_partials(ctx, ix, tb->D);
+    if (rc) return rc;
+    if (flags & DLRM_STEP_APPLY_ONLY) {
+        rc = DLRM_OK;
+    } else if (ix->split) {
+        CHECK_ARG((uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && dx_ld % 4 == 0 && dt_ld % 4 == 0,
+                  "dlrm_step_bwd: dx and dt must be 16-B aligned with leading dimensions divisible by 4");
+        rc = launch_step_bwd(ctx, tb->d_desc, tb->T, tb->dtype, indices, itype, table_stride, index_base, d, batch, x,
+                             x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, ix->dev, lr);
+    } else {
+        rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                        index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, nullptr);
+    }
+    if (rc || (flags & DLRM_STEP_BWD_ONLY)) return rc;
+    return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, 1, (int64_t)batch, dt,
+                            DLRM_F32, dt_ld, d, lr);
 }
 
 }  // extern "C"

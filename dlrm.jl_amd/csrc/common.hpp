@@ -10,7 +10,7 @@ namespace dlrm {
 constexpr int kWave = 64;  // CDNA wavefront
 
 // Device-side descriptor of one embedding table (SimpleEmbedding{Static{D}}.data).
-struct TableDesc {
+struct __attribute__((aligned(16))) TableDesc {
     void* data;     // [nrows][dim] row-major, f32 or bf16
     int64_t nrows;
 };
@@ -38,8 +38,42 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
+// Global-address-space accesses.  Pointers that come out of memory (TableDesc::data, kernel
+// argument structs) are generic to the compiler, which then emits flat_* instructions: those
+// count against both vmcnt and lgkmcnt, so every wait for one of them also drains LDS traffic.
+// Casting to address space 1 gives global_* instructions.
+#define DLRM_GLOBAL __attribute__((address_space(1)))
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename V> __device__ __forceinline__ V ldg(const void* p) { return *(const DLRM_GLOBAL V*)p; }
+template <typename V> __device__ __forceinline__ void stg(void* p, const V& v) { *(DLRM_GLOBAL V*)p = v; }
+#else  // host pass of the device code: never executed
+template <typename V> __device__ __forceinline__ V ldg(const void* p) { return *(const V*)p; }
+template <typename V> __device__ __forceinline__ void stg(void* p, const V& v) { *(V*)p = v; }
+#endif
+
+// Index i of an int32 / int64 index array, without a branch on the type: a branch per load
+// makes the compiler wait for each load at the join, serialising a lane's index loads.
+// (int32: the second word read is the first one again.)
 __device__ __forceinline__ int64_t load_index(const void* idx, int itype, int64_t i) {
-    return itype == DLRM_I64 ? ((const int64_t*)idx)[i] : (int64_t)((const int32_t*)idx)[i];
+    const uint32_t* p = (const uint32_t*)idx + (i << itype);
+    const uint32_t lo = ldg<uint32_t>(p), hi = ldg<uint32_t>(p + itype);
+    return itype ? (int64_t)(((uint64_t)hi << 32) | lo) : (int64_t)(int32_t)lo;
+}
+
+// One 16-B load (the compiler would otherwise sink the nrows half into the branch that tests it).
+__device__ __forceinline__ TableDesc load_table(const TableDesc* tabs, int t) {
+    const uint4 v = ldg<uint4>(tabs + t);
+    TableDesc d;
+    d.data = (void*)(((uint64_t)v.y << 32) | v.x);
+    d.nrows = (int64_t)(((uint64_t)v.w << 32) | v.z);
+    return d;
+}
+
+// load_index where the position may be invalid: the load always executes (at position 0) and
+// the result is masked, so no branch surrounds it.
+__device__ __forceinline__ int64_t load_index_if(bool ok, const void* idx, int itype, int64_t i) {
+    const int64_t v = load_index(idx, itype, ok ? i : 0);
+    return ok ? v : 0;
 }
 
 // 16-byte vector types
@@ -75,6 +109,33 @@ template <typename T> __device__ __forceinline__ T from_f32(float v);
 template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ uint16_t from_f32<uint16_t>(float v) { return f32_to_bf16(v); }
 
+// NE consecutive elements of a row as fp32 (16-B vector accesses where the size allows).
+template <typename TT, int NE>
+__device__ __forceinline__ void load_row(const TT* row, int c0, float* f) {
+    constexpr int BYTES = (int)sizeof(TT) * NE;
+    if constexpr (BYTES % 16 == 0) {
+        typedef Vec<TT> V;
+#pragma unroll
+        for (int k = 0; k < BYTES / 16; ++k) V::to_f32(ldg<typename V::type>((const typename V::type*)(row + c0) + k), f + k * V::N);
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) f[e] = to_f32(ldg<TT>(row + c0 + e));
+    }
+}
+
+template <typename TT, int NE>
+__device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
+    constexpr int BYTES = (int)sizeof(TT) * NE;
+    if constexpr (BYTES % 16 == 0) {
+        typedef Vec<TT> V;
+#pragma unroll
+        for (int k = 0; k < BYTES / 16; ++k) stg<typename V::type>((typename V::type*)(row + c0) + k, V::from_f32(f + k * V::N));
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) stg<TT>(row + c0 + e, from_f32<TT>(f[e]));
+    }
+}
+
 }  // namespace dlrm
 
 namespace dlrm {
@@ -91,6 +152,7 @@ struct IndexerDev {
     int32_t* hot_cnt;      // arrivals per hot segment (multi-slice combine; reset by the last)
     float* partial;        // [T][pcap][pdim] slice partial sums (multi-slice hot segments)
     int32_t* counts;       // [T][8]: U, chunks, hot, slices, nvalid
+    uint8_t* single;       // [T][cap]: 1 = the position's row is hit once in the batch (split builds)
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)
     int pdim;              // partial row capacity (elements)
@@ -122,6 +184,13 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
                                int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix);
+int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype, const void* idx,
+                    int itype, int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, void* out,
+                    int64_t out_ld, int padding, const IndexerDev& ix);
+int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T, int dtype, const void* idx, int itype,
+                    int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, const void* dout,
+                    int64_t dout_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev& ix,
+                    float lr);
 int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,

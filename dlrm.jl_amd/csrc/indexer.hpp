@@ -131,6 +131,7 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
         if (ok[j] && (peers & lt) == 0) sl.cnt[d][w] = (uint16_t)(base + __popcll(peers));
     }
     __syncthreads();
+    if (first) PHASE(2);
     // (digit, wave) offsets: thread tid owns the CPT counters [CPT tid, CPT tid + CPT) of cnt
     // in (digit, wave) order; one block scan over the per-thread sums
     uint32_t cw[CPT / 2];  // CPT uint16 counters, two per word
@@ -174,6 +175,7 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
         sl.maxbucket = 0;
     }
     __syncthreads();
+    if (first) PHASE(3);
     if (first) {
         // largest bucket (decides rank sort vs more passes)
         int m = 0;
@@ -181,6 +183,7 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
         if (lane == 0 && m > 0) atomicMax(&sl.maxbucket, m);
+        PHASE(4);
     }
 #pragma unroll
     for (int j = 0; j < EPL; ++j)
@@ -194,7 +197,9 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
     return total;
 }
 
-template <int NT, int EPL>
+// SPLIT (the training step's build, run before a backward that updates once-hit rows itself):
+// segments of one position get no chunk, and single[p] = 1 marks each such position p.
+template <int NT, int EPL, bool SPLIT = false>
 __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, const void* __restrict__ idx,
                                  int itype, int64_t tstride, int base, int N, unsigned* __restrict__ err,
                                  FastLds<NT, EPL>& sl) {
@@ -333,6 +338,14 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
             ++s;
         }
     if (tid == 0) seg_start[U] = n;
+    if (SPLIT) {  // once-hit positions: head of a segment whose next entry starts another
+        uint8_t* single = ix.single + off;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            const int i = EPL * tid + q;
+            if (i < n) single[Vs[i]] = (head[q] && (i + 1 == n || K[i + 1] != kq[q])) ? 1 : 0;
+        }
+    }
     __syncthreads();
     PHASE(20);
     // packed counts (N <= 4096 < 2^21): chunks bits 0-20, hot segments 21-41, hot slices 42-62
@@ -347,7 +360,8 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
             beg[q] = sseg[sidx];
             end[q] = sidx + 1 < U ? sseg[sidx + 1] : n;
             const int len = end[q] - beg[q];
-            cw += len <= kChunk ? 1ll : ((1ll << 21) | ((long long)((len + kHotSlice - 1) / kHotSlice) << 42));
+            if (!(SPLIT && len == 1))
+                cw += len <= kChunk ? 1ll : ((1ll << 21) | ((long long)((len + kHotSlice - 1) / kHotSlice) << 42));
         }
     }
     long long tot64;
@@ -361,7 +375,9 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
         const int sidx = EPL * tid + q;
         if (sidx < U) {
             const int len = end[q] - beg[q];
-            if (len <= kChunk) {
+            if (SPLIT && len == 1) {
+                // updated by the backward (single[] flag)
+            } else if (len <= kChunk) {
                 chunks[c++] = make_int4(beg[q], end[q], (int)srow[sidx], Vs[beg[q]]);
             } else {
                 const int ns = (len + kHotSlice - 1) / kHotSlice;

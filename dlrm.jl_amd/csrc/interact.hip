@@ -23,8 +23,22 @@
 // B fragments are rows of T read straight from HBM (16 consecutive floats per 16 lanes).
 // The interaction's arithmetic intensity (~11-24 flop/B) is far below the MFMA ridge, so
 // these kernels are HBM-bound; MFMA just keeps the VALU free and the operand traffic low.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "indexer.hpp"
+
+#ifdef DLRM_WTRACE
+// Per-sample wave timestamps (wall_clock64, 100 MHz) of the forward (kind 0) and backward
+// (kind 1) bodies; only in the tracing build (tools/wave_trace.sh).
+__device__ unsigned long long g_wt[2][6][8192];
+#define WT(kind, slot, b) do { if ((threadIdx.x & 63) == 0 && (b) < 8192) g_wt[kind][slot][b] = wall_clock64(); } while (0)
+extern "C" int dlrm_debug_wtrace(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wt), sizeof(g_wt));
+}
+#else
+#define WT(kind, slot, b) do {} while (0)
+#endif
 
 namespace dlrm {
 
@@ -95,53 +109,50 @@ struct GatherArgs {
     unsigned* err;
 };
 
-template <typename T, int NB, bool FUSED, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
-                                                                int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
-                                                                T* __restrict__ out, int64_t out_ld, int padding,
-                                                                GatherArgs ga) {
+// Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
+template <typename T, int NB, bool FUSED, int WPB, bool POOL = false>
+__device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all, int d, int F, int B,
+                                         const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
+                                         T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga) {
     typedef Frag<T> FR;
     typedef typename FR::type frag;
     constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
-    __shared__ float stage_all[WPB][kStage];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 15, q = lane >> 4;
     const int P = F * (F - 1) / 2;
     const int W = d + P + padding;
     const bool staged = W <= kStage;
-    float* stage = stage_all[w];
-    for (int64_t b = (int64_t)blockIdx.x * WPB + w; b < B; b += (int64_t)gridDim.x * WPB) {
+    float* stage = stage_all + w * kStage;
+    for (int64_t b = (int64_t)bid * WPB + w; b < B; b += (int64_t)nblocks * WPB) {
+        WT(0, 0, b);
         const T* xb = x + b * x_ld;
         T* yb = ys ? ys + b * ys_ld : nullptr;  // FUSED: ys may be NULL (not materialized)
         T* orow = out + b * out_ld;
         // fast_vcat: x into the reserved rows of ys; x is also the head of the output row.
         for (int i = lane; i < d; i += 64) {
-            const T v = xb[i];
-            if (yb) yb[i] = v;
+            const T v = ldg<T>(xb + i);
+            if (yb) stg<T>(yb + i, v);
             if (staged) stage[i] = to_f32(v);
-            else orow[i] = v;
+            else stg<T>(orow + i, v);
         }
-        // row sources: feature 0 is x itself; features 1..F-1 are ys rows or table rows
+        // row sources: feature 0 is x itself; features 1..F-1 are ys rows or table rows.  Every
+        // load below executes unconditionally (invalid slots read x and are masked to zero), so
+        // no branch makes the compiler wait for a lane's loads one at a time.
         const T* src[NB];
         int64_t kidx[NB];  // FUSED, pooled: index position of lookup 0 of this (table, sample)
+        TableDesc td[NB];
 #pragma unroll
         for (int I = 0; I < NB; ++I) {
             const int row = I * 16 + c;
-            src[I] = nullptr;
-            kidx[I] = -1;
-            if (row == 0) {
-                src[I] = xb;
-            } else if (row < F) {
-                if (!FUSED) {
-                    src[I] = yb + (int64_t)row * d;
-                } else {
-                    const int t = row - 1;
-                    kidx[I] = t * ga.tstride + b * ga.L;
-                    const int64_t r = load_index(ga.idx, ga.itype, kidx[I]) - ga.base;
-                    if (r >= 0 && r < ga.tabs[t].nrows) src[I] = (const T*)ga.tabs[t].data + r * d;
-                    else if (q == 0) raise_index_error(ga.err);
-                }
-            }
+            const bool tab = FUSED && row >= 1 && row < F;
+            kidx[I] = tab ? (row - 1) * ga.tstride + b * ga.L : -1;
+            td[I] = FUSED ? load_table(ga.tabs, tab ? row - 1 : 0) : TableDesc{};
+            const int64_t r = load_index_if(tab, ga.idx, ga.itype, kidx[I]) - ga.base;
+            const bool ok = tab & (r >= 0) & (r < td[I].nrows);
+            if (tab & !ok & (q == 0)) raise_index_error(ga.err);
+            src[I] = row == 0 ? xb
+                              : (!FUSED ? (row < F ? yb + (int64_t)row * d : nullptr)
+                                        : (ok ? (const T*)td[I].data + r * d : nullptr));
         }
         f32x4_t acc[NB * (NB + 1) / 2];
 #pragma unroll
@@ -152,28 +163,33 @@ __global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, in
             for (int uu = 0; uu < UU; ++uu) {
                 const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
 #pragma unroll
-                for (int I = 0; I < NB; ++I)
-                    a[uu][I] = (src[I] && col < d) ? *(const frag*)(src[I] + col) : FR::zero();
+                for (int I = 0; I < NB; ++I) {
+                    const bool ok = src[I] && col < d;
+                    const frag v = ldg<frag>((ok ? src[I] : xb) + (ok ? col : 0));
+                    a[uu][I] = ok ? v : FR::zero();
+                }
             }
             if (FUSED) {
                 // pooled bags: add lookups 1..L-1 in k order (fp32), round once to T
-                if (ga.L > 1) {
+                if (POOL && ga.L > 1) {
 #pragma unroll
                     for (int I = 0; I < NB; ++I) {
-                        if (kidx[I] < 0) continue;
-                        const int t = I * 16 + c - 1;
+                        const bool tab = kidx[I] >= 0;
                         float f[UU][FR::PER_LANE];
 #pragma unroll
                         for (int uu = 0; uu < UU; ++uu) FR::to_f(f[uu], a[uu][I]);
+#pragma unroll 4
                         for (int k = 1; k < ga.L; ++k) {
-                            const int64_t r = load_index(ga.idx, ga.itype, kidx[I] + k) - ga.base;
-                            const T* rp = nullptr;
-                            if (r >= 0 && r < ga.tabs[t].nrows) rp = (const T*)ga.tabs[t].data + r * d;
-                            else if (q == 0 && u0 == 0) raise_index_error(ga.err);
+                            const int64_t r = load_index_if(tab, ga.idx, ga.itype, kidx[I] + k) - ga.base;
+                            const bool ok = tab & (r >= 0) & (r < td[I].nrows);
+                            if (tab & !ok & (q == 0) & (u0 == 0)) raise_index_error(ga.err);
+                            const T* rp = ok ? (const T*)td[I].data + r * d : xb;
 #pragma unroll
                             for (int uu = 0; uu < UU; ++uu) {
                                 const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
-                                if (rp && col < d) FR::add_to(f[uu], *(const frag*)(rp + col));
+                                const bool okc = ok && col < d;
+                                const frag v = ldg<frag>(rp + (okc ? col : 0));
+                                FR::add_to(f[uu], okc ? v : FR::zero());
                             }
                         }
 #pragma unroll
@@ -188,7 +204,7 @@ __global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, in
 #pragma unroll
                     for (int I = 0; I < NB; ++I) {
                         const int row = I * 16 + c;
-                        if (row >= 1 && row < F && col < d) *(frag*)(yb + (int64_t)row * d + col) = a[uu][I];
+                        if (row >= 1 && row < F && col < d) stg<frag>(yb + (int64_t)row * d + col, a[uu][I]);
                     }
                 }
             }
@@ -201,6 +217,7 @@ __global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, in
                     for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[ij], a[uu][I], a[uu][J]);
             }
         }
+        WT(0, 1, b);
         // Z[i][j], i > j: triangular_slice_kernel! order (i-major), after x
         {
             int ij = 0;
@@ -215,21 +232,55 @@ __global__ __launch_bounds__(64 * WPB) void interact_fwd_kernel(int d, int F, in
                         if (i < F && j < i) {
                             const int e = d + i * (i - 1) / 2 + j;
                             if (staged) stage[e] = acc[ij][r];
-                            else orow[e] = from_f32<T>(acc[ij][r]);
+                            else stg<T>(orow + e, from_f32<T>(acc[ij][r]));
                         }
                     }
                 }
         }
         for (int e = d + P + lane; e < W; e += 64) {
             if (staged) stage[e] = 0.0f;
-            else orow[e] = from_f32<T>(0.0f);
+            else stg<T>(orow + e, from_f32<T>(0.0f));
         }
         if (staged) {
             wave_lds_sync();
-            for (int e = lane; e < W; e += 64) orow[e] = from_f32<T>(stage[e]);
+            for (int e = lane; e < W; e += 64) stg<T>(orow + e, from_f32<T>(stage[e]));
             wave_lds_sync();
         }
+        WT(0, 2, b);
     }
+}
+
+// POOL: the pooled-bag path (lookups > 1) is compiled in; the one-hot kernel stays lean.
+template <typename T, int NB, bool FUSED, bool POOL, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
+                                                                   int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
+                                                                   T* __restrict__ out, int64_t out_ld, int padding,
+                                                                   GatherArgs ga) {
+    __shared__ float stage_all[WPB * kStage];
+    fwd_body<T, NB, FUSED, WPB, POOL>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding,
+                                ga);
+}
+
+// The forward of a training step with the SparseIndexer build in the same grid (split form:
+// once-hit positions flagged for the backward, the rest listed for the apply): workgroups
+// [0, T) each sort one table's positions (indexer.hpp, 256 threads), the rest run the fused
+// lookup + interaction without ys.  The indexer depends only on the indices, so it streams
+// beside the gather instead of adding a launch.
+constexpr int kStepIndexEPL = 8;  // positions per thread: N <= 2048
+template <typename T, int NB>
+__global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F, int B, const T* __restrict__ x,
+                                                                 int64_t x_ld, T* __restrict__ out, int64_t out_ld,
+                                                                 int padding, GatherArgs ga, IndexerDev ix) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int T_ = F - 1;
+    if ((int)blockIdx.x < T_) {
+        FastLds<256, kStepIndexEPL>& sl = *(FastLds<256, kStepIndexEPL>*)smem;
+        fast_index_table<256, kStepIndexEPL, true>(ix, blockIdx.x, (uint32_t)ga.tabs[blockIdx.x].nrows, ga.idx,
+                                                   ga.itype, ga.tstride, ga.base, B * ga.L, ga.err, sl);
+        return;
+    }
+    fwd_body<T, NB, true, 4>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, x, x_ld, nullptr, 0, out, out_ld, padding,
+                             ga);
 }
 
 // ---------------------------------------------------------------------------------- bwd
@@ -237,13 +288,15 @@ template <int NB> struct BwdGeom {
     static constexpr int NS = 16 * NB;                          // padded features
     static constexpr int SS = NS + ((NB % 2 == 0) ? 16 : 0);    // row stride = 16 (mod 32)
     static constexpr int WPB = NB <= 2 ? 4 : (NB <= 4 ? 2 : 1); // waves per block
-    static constexpr int LDS_FLOATS = NS * SS;                  // per wave
+    static constexpr int LDS_FLOATS = NS * SS;                  // per wave: S
+    // per wave, with the UPD T tile ([NS][64] floats of one super-block) after S
+    template <bool UPD> static constexpr int lds_floats() { return NS * SS + (UPD ? NS * 64 : 0); }
 };
 
 // 4 consecutive elements of T as fp32 (16-B load for fp32, 8-B for bf16)
-__device__ __forceinline__ f32x4_t load4_f32(const float* p) { return *(const f32x4_t*)p; }
+__device__ __forceinline__ f32x4_t load4_f32(const float* p) { return ldg<f32x4_t>(p); }
 __device__ __forceinline__ f32x4_t load4_f32(const uint16_t* p) {
-    const uint2 v = *(const uint2*)p;
+    const uint2 v = ldg<uint2>(p);
     return f32x4_t{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
                    __uint_as_float(v.y & 0xffff0000u)};
 }
@@ -255,105 +308,214 @@ __device__ __forceinline__ f32x4_t load4_f32(const uint16_t* p) {
 // All k-step loads of a super-block are issued before its MFMAs (up to 4*NB in flight).
 // GATHER: T_b is not read from a materialized ys but rebuilt from x (row 0) and the table
 // rows of the sample's one-hot indices (rows 1..F-1): the same values, without ys.
-template <typename T, int NB, bool GATHER>
+// UPD (training step, split indexer): a table row hit by this sample only (single[] flag of
+// the forward's indexer build) gets its SGD step here -- w = fmaf(-lr, 0 + g, w), exactly the
+// apply kernel's arithmetic for a one-position segment -- and its dt row is not written.  No
+// other sample reads that row, so the in-place update cannot race with another wave's gather.
+struct StepUpdate {
+    const uint8_t* single;  // [T][cap]
+    int64_t cap;
+    float lr;
+};
+
+template <typename T, int NB, bool GATHER, bool UPD = false, int SBU_ = 0>
 __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int d, int F, int B,
                                          const T* __restrict__ dout, int64_t dout_ld, const T* __restrict__ t,
                                          int64_t t_ld, float* __restrict__ dx, int64_t dx_ld,
                                          float* __restrict__ dt, int64_t dt_ld, const GatherArgs& ga,
-                                         const T* __restrict__ x, int64_t x_ld) {
+                                         const T* __restrict__ x, int64_t x_ld, const StepUpdate& su = StepUpdate{}) {
     typedef BwdGeom<NB> G;
-    constexpr int KS = 4 * NB;  // max k-steps (F <= 16 NB)
+    constexpr int KS = 4 * NB;          // max k-steps (F <= 16 NB)
+    constexpr int SBU = SBU_ > 0 ? SBU_ : (NB <= 2 ? 2 : 1);  // 64-column super-blocks loaded together
+    constexpr int KPB = 8;              // packed-gradient values per lane loaded together
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the table descriptors, once per workgroup, in LDS after the waves' regions: read where
+    // used instead of held in registers across the index loads
+    TableDesc* tds = (TableDesc*)(smem + G::WPB * G::template lds_floats<UPD>());
+    if (GATHER) {
+        for (int t = threadIdx.x; t < F - 1; t += blockDim.x) tds[t] = load_table(ga.tabs, t);
+        __syncthreads();
+    }
     if (w >= G::WPB) return;
     const int c = lane & 15, q = lane >> 4;
-    float* S = smem + w * G::LDS_FLOATS;
+    float* S = smem + w * G::template lds_floats<UPD>();
+    float* Tt = S + G::NS * G::SS;  // UPD: the current super-block of T, [NS][64]
     const int P = F * (F - 1) / 2;
     const int ksteps = (F + 3) / 4;
     for (int64_t b = (int64_t)bid * G::WPB + w; b < B; b += (int64_t)nblocks * G::WPB) {
+        WT(1, 0, b);
         const T* ob = dout + b * dout_ld;
         const T* tb = GATHER ? nullptr : t + b * t_ld;
+        // Independent loads first, so their latencies overlap: the sample's indices (T rows and,
+        // UPD, the once-hit flags of its output rows) and the first packed-gradient values.
         const T* rowp[KS];  // GATHER: this lane's T rows kk = 4s + q
         if (GATHER) {
+            int64_t ri[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const int kk = 4 * s + q;
-                rowp[s] = nullptr;
-                if (s < ksteps && kk < F) {
-                    if (kk == 0) {
-                        rowp[s] = x + b * x_ld;
-                    } else {
-                        const int64_t r = load_index(ga.idx, ga.itype, (kk - 1) * ga.tstride + b * ga.L) - ga.base;
-                        if (r >= 0 && r < ga.tabs[kk - 1].nrows) rowp[s] = (const T*)ga.tabs[kk - 1].data + r * d;
-                        else if (c == 0) raise_index_error(ga.err);
-                    }
-                }
+                const bool tab = s < ksteps && kk >= 1 && kk < F;
+                ri[s] = load_index_if(tab, ga.idx, ga.itype, (kk - 1) * ga.tstride + b * ga.L);
             }
-        }
-        // S: zero, then scatter the packed pairs to both triangles (fused unpack + transpose-add)
-        for (int e = lane; e < G::NS * G::NS; e += 64) S[(e / G::NS) * G::SS + (e % G::NS)] = 0.0f;
-        wave_lds_sync();
-        for (int p = lane; p < P; p += 64) {
-            int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)p)) * 0.5f);
-            while (i * (i - 1) / 2 > p) --i;
-            while ((i + 1) * i / 2 <= p) ++i;
-            const int j = p - i * (i - 1) / 2;
-            const float v = to_f32(ob[d + p]);
-            S[i * G::SS + j] = v;
-            S[j * G::SS + i] = v;
-        }
-        wave_lds_sync();
-        for (int sb = 0; sb < d; sb += 64) {
-            const int n0 = sb + 4 * c;  // this lane's 4 output columns
-            const bool colok = n0 < d;
-            f32x4_t bv[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const int kk = 4 * s + q;
-                const T* src = GATHER ? rowp[s] : (kk < F ? tb + (int64_t)kk * d : nullptr);
-                bv[s] = (s < ksteps && src && colok) ? load4_f32(src + n0) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+                const bool tab = s < ksteps && kk >= 1 && kk < F;
+                const TableDesc td = tds[tab ? kk - 1 : 0];
+                const int64_t r = ri[s] - ga.base;
+                const bool ok = tab & (r >= 0) & (r < td.nrows);
+                if (tab & !ok & (c == 0)) raise_index_error(ga.err);
+                rowp[s] = (s < ksteps && kk == 0) ? x + b * x_ld : (ok ? (const T*)td.data + r * d : nullptr);
             }
-            f32x4_t acc[NB][4];
+        }
+        T* urow[NB][4];  // UPD: the once-hit table row of output row f = 16I + 4q + r, else null
+        if (UPD) {
+            uint8_t fl[NB][4];
+            int64_t ui[NB][4];
 #pragma unroll
             for (int I = 0; I < NB; ++I)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                for (int r = 0; r < 4; ++r) {
+                    const int f = I * 16 + 4 * q + r;
+                    const bool tab = f >= 1 && f < F;
+                    fl[I][r] = ldg<uint8_t>(su.single + (tab ? (int64_t)(f - 1) * su.cap + b : 0));
+                    ui[I][r] = load_index_if(tab, ga.idx, ga.itype, (f - 1) * ga.tstride + b);
+                }
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                if (s < ksteps) {
-                    const int kk = 4 * s + q;
+            for (int I = 0; I < NB; ++I)
 #pragma unroll
-                    for (int I = 0; I < NB; ++I) {
-                        const float av = S[kk * G::SS + I * 16 + c];  // = S[16I+c][kk] (symmetric)
+                for (int r = 0; r < 4; ++r) {
+                    const int f = I * 16 + 4 * q + r;
+                    const bool tab = f >= 1 && f < F;
+                    const TableDesc td = tds[tab ? f - 1 : 0];
+                    const int64_t rr = ui[I][r] - ga.base;
+                    urow[I][r] = (tab & (fl[I][r] != 0) & (rr >= 0) & (rr < td.nrows)) ? (T*)td.data + rr * d
+                                                                                       : nullptr;
+                }
+        }
+        // The first super-blocks' T rows (and dout's x part) go out before S is built, so their
+        // latency overlaps the packed-gradient loads and the LDS scatter.
+        f32x4_t bv[SBU][KS];
+        f32x4_t xo[SBU];
+        // every lane's T row pointer is valid (ob, the dout row, stands in for a missing row) and
+        // `live` masks the values, so the loads are plain base + offset with no selects
+        unsigned live = 0;
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s][e], acc[I][e], 0, 0, 0);
-                    }
+        for (int s = 0; s < KS; ++s) {
+            const int kk = 4 * s + q;
+            const T* src = GATHER ? rowp[s] : (kk < F ? tb + (int64_t)kk * d : nullptr);
+            live |= (s < ksteps && src) ? (1u << s) : 0u;
+            rowp[s] = (s < ksteps && src) ? src : ob;
+        }
+        auto load_batch = [&](int sb0) {
+#pragma unroll
+            for (int h = 0; h < SBU; ++h) {
+                const int n0 = sb0 + 64 * h + 4 * c;
+                const int nc = n0 < d ? n0 : 0;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const f32x4_t v = load4_f32(rowp[s] + nc);
+                    bv[h][s] = ((live >> s) & 1u) && n0 < d ? v : f32x4_t{0.f, 0.f, 0.f, 0.f};
+                }
+                const int nx = n0 < d ? n0 : 0;  // dout rows need no alignment: scalar reads
+                xo[h] = f32x4_t{to_f32(ldg<T>(ob + nx)), to_f32(ldg<T>(ob + nx + 1)), to_f32(ldg<T>(ob + nx + 2)),
+                                to_f32(ldg<T>(ob + nx + 3))};
+            }
+        };
+        load_batch(0);
+        // S: zero, then scatter the packed pairs to both triangles (fused unpack + transpose-add);
+        // KPB values per lane in flight
+        for (int e = lane; e < G::NS * G::NS; e += 64) S[(e / G::NS) * G::SS + (e % G::NS)] = 0.0f;
+        wave_lds_sync();
+        for (int p0 = 0; p0 < P; p0 += 64 * KPB) {
+            float dv[KPB];
+#pragma unroll
+            for (int k = 0; k < KPB; ++k) {
+                const int p = p0 + 64 * k + lane;
+                const float v = to_f32(ldg<T>(ob + d + (p < P ? p : 0)));
+                dv[k] = p < P ? v : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < KPB; ++k) {
+                const int p = p0 + 64 * k + lane;
+                if (p < P) {
+                    int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)p)) * 0.5f);
+                    while (i * (i - 1) / 2 > p) --i;
+                    while ((i + 1) * i / 2 <= p) ++i;
+                    const int j = p - i * (i - 1) / 2;
+                    S[i * G::SS + j] = dv[k];
+                    S[j * G::SS + i] = dv[k];
                 }
             }
-            if (colok) {
+        }
+        wave_lds_sync();
+        WT(1, 1, b);
+        for (int sb0 = 0; sb0 < d; sb0 += 64 * SBU) {
+            if (sb0 > 0) load_batch(sb0);
+#pragma unroll
+            for (int h = 0; h < SBU; ++h) {
+                const int sb = sb0 + 64 * h;
+                if (sb >= d) break;
+                const int n0 = sb + 4 * c;  // this lane's 4 output columns
+                const bool colok = n0 < d;
+                if (UPD) {  // stage the super-block's T rows: the update needs row f where dt row f is
+                    wave_lds_sync();
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        const int kk = 4 * s + q;
+                        if (s < ksteps && kk < F) *(f32x4_t*)(Tt + kk * 64 + 4 * c) = bv[h][s];
+                    }
+                    wave_lds_sync();
+                }
+                f32x4_t acc[NB][4];
 #pragma unroll
                 for (int I = 0; I < NB; ++I)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int f = I * 16 + 4 * q + r;
-                        if (f < F) {
-                            const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
-                            *(f32x4_t*)(dt + b * dt_ld + (int64_t)f * d + n0) = v;
-                            if (f == 0) {  // dout rows need no alignment: scalar reads
-                                const f32x4_t xo = f32x4_t{to_f32(ob[n0]), to_f32(ob[n0 + 1]), to_f32(ob[n0 + 2]),
-                                                           to_f32(ob[n0 + 3])};
-                                *(f32x4_t*)(dx + b * dx_ld + n0) = xo + v;
-                            }
+                    for (int e = 0; e < 4; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    if (s < ksteps) {
+                        const int kk = 4 * s + q;
+#pragma unroll
+                        for (int I = 0; I < NB; ++I) {
+                            const float av = S[kk * G::SS + I * 16 + c];  // = S[16I+c][kk] (symmetric)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[h][s][e], acc[I][e], 0, 0, 0);
                         }
                     }
+                }
+                if (sb < 128) WT(1, 2 + sb / 64, b);
+                if (colok) {
+#pragma unroll
+                    for (int I = 0; I < NB; ++I)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int f = I * 16 + 4 * q + r;
+                            if (f < F) {
+                                const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
+                                if (UPD && urow[I][r]) {
+                                    const f32x4_t tw = *(const f32x4_t*)(Tt + f * 64 + 4 * c);
+                                    float wv[4];
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
+                                    store_row<T, 4>(urow[I][r], n0, wv);
+                                } else {
+                                    stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+                                }
+                                if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo[h] + v);
+                            }
+                        }
+                }
             }
         }
+        WT(1, 4, b);
         wave_lds_sync();
     }
 }
 
 template <typename T, int NB, bool GATHER>
-__global__ __launch_bounds__(256) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
+__global__ __launch_bounds__(256, 2) void interact_bwd_kernel(int d, int F, int B, const T* __restrict__ dout,
                                                            int64_t dout_ld, const T* __restrict__ t, int64_t t_ld,
                                                            float* __restrict__ dx, int64_t dx_ld,
                                                            float* __restrict__ dt, int64_t dt_ld, GatherArgs ga,
@@ -383,8 +545,22 @@ __global__ __launch_bounds__(256, 3) void interact_bwd_index_kernel(int d, int F
                                             ga.tstride, ga.base, B * ga.L, ga.err, sl);
         return;
     }
-    bwd_body<T, NB, true>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
+    bwd_body<T, NB, true, false, 1>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
                           dt_ld, ga, x, x_ld);
+}
+
+// The backward of a training step after interact_fwd_index_kernel: re-gathers T, writes dx
+// and the dt rows of positions whose row is hit more than once, and applies the SGD step to
+// once-hit rows itself (the apply launch that follows handles the rest).
+template <typename T, int NB, int SBU>
+__global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int F, int B, const T* __restrict__ dout,
+                                                                  int64_t dout_ld, float* __restrict__ dx,
+                                                                  int64_t dx_ld, float* __restrict__ dt, int64_t dt_ld,
+                                                                  GatherArgs ga, const T* __restrict__ x, int64_t x_ld,
+                                                                  StepUpdate su) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    bwd_body<T, NB, true, true, SBU>(blockIdx.x, gridDim.x, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
+                                     dt_ld, ga, x, x_ld, su);
 }
 
 // ------------------------------------------------------------------ scalar fallbacks
@@ -466,8 +642,12 @@ template <typename T, int NB, bool FUSED>
 static void launch_fwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
                           int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
     const unsigned g = grid_for(B, 4, cus);
-    hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x, x_ld,
-                       (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+    if (FUSED && ga.L > 1)
+        hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, true>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
+                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+    else
+        hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, false>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
+                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
 }
 
 template <typename T, bool FUSED>
@@ -523,7 +703,7 @@ int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
     if (B == 0) return DLRM_OK;
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
-    if (!tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, ys, ys_ld) || NB > 6) return DLRM_E_UNSUPPORTED;
+    if (T_ == 0 || !tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, ys, ys_ld) || NB > 6) return DLRM_E_UNSUPPORTED;
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
@@ -540,7 +720,7 @@ static void launch_bwd_nb(hipStream_t s, int cus, int d, int F, int B, const voi
                           const GatherArgs& ga, const void* x, int64_t x_ld) {
     typedef BwdGeom<NB> G;
     const unsigned g = grid_for(B, G::WPB, cus);
-    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB;
+    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB + (GATHER ? sizeof(TableDesc) * (F - 1) : 0);
     hipLaunchKernelGGL((interact_bwd_kernel<T, NB, GATHER>), dim3(g), dim3(64 * G::WPB), lds, s, d, F, B,
                        (const T*)dout, dout_ld, (const T*)t, t_ld, dx, dx_ld, dt, dt_ld, ga, (const T*)x, x_ld);
 }
@@ -617,7 +797,7 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
 #define DLRM_LAUNCH_BWDIX(TY, N_)                                                                                 \
     {                                                                                                              \
         typedef BwdGeom<N_> G;                                                                                     \
-        const size_t blds = sizeof(float) * G::LDS_FLOATS * G::WPB;                                                \
+        const size_t blds = sizeof(float) * G::LDS_FLOATS * G::WPB + sizeof(TableDesc) * T_;                       \
         if (blds > lds) lds = blds;                                                                                \
         const unsigned g = grid_for(B, G::WPB, cus);                                                               \
         hipLaunchKernelGGL((interact_bwd_index_kernel<TY, N_>), dim3(g + T_), dim3(256), lds, s, d, F, B,          \
@@ -637,6 +817,72 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
     }
     return run_interact_bwd<true>(ctx, dtype, d, T_ + 1, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt, dt_ld, ga,
                                   tabs_aligned16, x, x_ld);
+}
+
+// Training-step forward (split indexer in the same grid).  DLRM_E_UNSUPPORTED when the shape
+// has no such kernel (the caller then runs the fused forward and the indexer separately).
+int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype, const void* idx,
+                    int itype, int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, void* out,
+                    int64_t out_ld, int padding, const IndexerDev& ix) {
+    const int F = T_ + 1;
+    const int NB = (F + 15) / 16;
+    if (B == 0 || T_ == 0 || !tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, nullptr, 0) || NB > 2 ||
+        B > 256 * kStepIndexEPL)
+        return DLRM_E_UNSUPPORTED;
+    hipStream_t s = ctx_stream(ctx);
+    const int cus = ctx_num_cus(ctx);
+    GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
+    size_t lds = sizeof(FastLds<256, kStepIndexEPL>);
+    if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
+    const unsigned g = grid_for(B, 4, cus) + T_;
+#define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
+    hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_>), dim3(g), dim3(256), lds, s, d, F, B, (const TY*)x, x_ld, \
+                       (TY*)out, out_ld, padding, ga, ix);
+    if (dtype == DLRM_F32) {
+        if (NB == 1) DLRM_LAUNCH_FWDIX(float, 1) else DLRM_LAUNCH_FWDIX(float, 2)
+    } else {
+        if (NB == 1) DLRM_LAUNCH_FWDIX(uint16_t, 1) else DLRM_LAUNCH_FWDIX(uint16_t, 2)
+    }
+#undef DLRM_LAUNCH_FWDIX
+    return ctx_hip(ctx, hipGetLastError(), "step_fwd launch");
+}
+
+// Training-step backward after launch_step_fwd: once-hit rows updated in place, dt rows of the
+// others written for the apply.  The caller checked the shape (launch_step_fwd accepted it)
+// and the 16-B alignment of dx / dt.
+int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, const void* idx, int itype,
+                    int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, const void* dout,
+                    int64_t dout_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev& ix,
+                    float lr) {
+    if (B == 0 || T_ == 0) return DLRM_OK;
+    const int F = T_ + 1;
+    const int NB = (F + 15) / 16;
+    hipStream_t s = ctx_stream(ctx);
+    const int cus = ctx_num_cus(ctx);
+    GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
+    StepUpdate su{ix.single, ix.cap, lr};
+    // one super-block of T rows in flight: two (the gather backward's choice) spill here
+    static const int sbu = getenv("DLRM_UPD_SBU") ? atoi(getenv("DLRM_UPD_SBU")) : 1;  // experiment knob
+#define DLRM_LAUNCH_BWDUP(TY, N_)                                                                                  \
+    {                                                                                                              \
+        typedef BwdGeom<N_> G;                                                                                     \
+        const size_t lds = sizeof(float) * G::template lds_floats<true>() * G::WPB + sizeof(TableDesc) * T_;       \
+        if (sbu == 2)                                                                                              \
+            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 2>), dim3(grid_for(B, G::WPB, cus)),             \
+                               dim3(64 * G::WPB), lds, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, \
+                               (const TY*)x, x_ld, su);                                                            \
+        else                                                                                                       \
+            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 1>), dim3(grid_for(B, G::WPB, cus)),             \
+                               dim3(64 * G::WPB), lds, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, \
+                               (const TY*)x, x_ld, su);                                                            \
+    }
+    if (dtype == DLRM_F32) {
+        if (NB == 1) DLRM_LAUNCH_BWDUP(float, 1) else DLRM_LAUNCH_BWDUP(float, 2)
+    } else {
+        if (NB == 1) DLRM_LAUNCH_BWDUP(uint16_t, 1) else DLRM_LAUNCH_BWDUP(uint16_t, 2)
+    }
+#undef DLRM_LAUNCH_BWDUP
+    return ctx_hip(ctx, hipGetLastError(), "step_bwd launch");
 }
 
 }  // namespace dlrm

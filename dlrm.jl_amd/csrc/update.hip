@@ -323,32 +323,6 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 }
 
 // ------------------------------------------------------------------------------ apply
-template <typename TT, int NE>
-__device__ __forceinline__ void load_row(const TT* row, int c0, float* f) {
-    constexpr int BYTES = (int)sizeof(TT) * NE;
-    if constexpr (BYTES % 16 == 0) {
-        typedef Vec<TT> V;
-#pragma unroll
-        for (int k = 0; k < BYTES / 16; ++k) V::to_f32(*((const typename V::type*)(row + c0) + k), f + k * V::N);
-    } else {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) f[e] = to_f32(row[c0 + e]);
-    }
-}
-
-template <typename TT, int NE>
-__device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
-    constexpr int BYTES = (int)sizeof(TT) * NE;
-    if constexpr (BYTES % 16 == 0) {
-        typedef Vec<TT> V;
-#pragma unroll
-        for (int k = 0; k < BYTES / 16; ++k) *((typename V::type*)(row + c0) + k) = V::from_f32(f + k * V::N);
-    } else {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) row[c0 + e] = from_f32<TT>(f[e]);
-    }
-}
-
 // Lane-group geometry: D elements = VPR vectors of 16 B of the GRAD dtype; a group of LPR
 // lanes owns one row, a wave holds RPW groups.
 template <typename GT, int VPR>
@@ -406,7 +380,6 @@ __device__ __forceinline__ void sum_positions(const int32_t* __restrict__ perm, 
 // by the segment length only); each stages its slice's positions in LDS with one cooperative
 // read, then sums the grad rows in position order with kHotInFlight rows in flight.  The
 // group partials are added in group order and the row is written once.
-constexpr int kHotStage = 128;   // positions staged per lane group per round
 constexpr int kHotInFlight = 8;   // grad rows in flight per lane group
 
 template <typename GT, int VPR>

@@ -9,8 +9,9 @@ does for the sparse half of the model on one batch:
     dx, dt = dot_back(dot, dout, T, d, padding)                    interact.jl:442-445
     update!(Descent(lr), tables, maplookup_pullback(dt), indexers) train.jl:283-290
 
-All buffers are allocated once; a step issues 4 kernel launches on the current stream
-(fused lookup + interaction fwd, indexer sort, interaction bwd, update) with no host
+All buffers are allocated once; a step issues 3 kernel launches on the current stream
+(default: dlrm_step_fwd = lookup + interaction + indexer sort; dlrm_step_bwd = interaction
+bwd with the SGD step of once-hit rows, then the apply of repeated rows) with no host
 synchronisation, so the whole step can be captured in a torch.cuda graph (`fused=False`
 runs maplookup and the interaction as two launches, like the reference).  With
 `overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a side
@@ -64,6 +65,9 @@ class HotPath:
         self.overlap_indexer = overlap_indexer and deterministic
         self._side = torch.cuda.Stream(device=dev) if self.overlap_indexer else None
         self._indexer_done = None
+        # the training-step pair (dlrm_step_fwd / dlrm_step_bwd): indexer built inside the forward's
+        # launch, once-hit rows updated inside the backward's, the rest by the apply launch
+        self.step_api = (not self.materialize_ys) and self.indexer is not None and not self.overlap_indexer
 
     # -- pieces --------------------------------------------------------------------------
     def _check(self, rc):
@@ -123,6 +127,25 @@ class HotPath:
                                              ptr(idx.data), idx.itype, idx.stride, self.index_base, self.B, self.L,
                                              ptr(self.dt), _lib.F32, self.dt.stride(0), self.d, self.lr))
 
+    def step_fwd(self, x, idx):
+        """dlrm_step_fwd: lookup + interaction (no ys) + the split indexer, one launch."""
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_step_fwd(h, self.ts.handle, self.indexer.handle, ptr(idx.data), idx.itype,
+                                           idx.stride, self.index_base, self.B, ptr(x), x.stride(0), ptr(self.out),
+                                           self.out.stride(0), self.padding))
+        self._fwd_x, self._fwd_idx = x, idx
+
+    def step_bwd(self, dout, x=None, idx=None, flags=0):
+        """dlrm_step_bwd: dot_back + update!(Descent(lr)) with the indexer of step_fwd
+        (flags: _lib.STEP_BWD_ONLY / STEP_APPLY_ONLY run one of its two launches)."""
+        h = self.ctx.bind()
+        x = self._fwd_x if x is None else x
+        idx = self._fwd_idx if idx is None else idx
+        self._check(self.lib.dlrm_step_bwd(h, self.ts.handle, self.indexer.handle, ptr(idx.data), idx.itype,
+                                           idx.stride, self.index_base, self.B, ptr(x), x.stride(0), ptr(dout),
+                                           dout.stride(0), self.padding, ptr(self.dx), self.dx.stride(0),
+                                           ptr(self.dt), self.dt.stride(0), self.lr, flags))
+
     # -- step --------------------------------------------------------------------------
     def validate(self, x, idx, dout=None):
         """Host-side shape/device checks (call once per new buffer set; the step itself does not)."""
@@ -139,6 +162,9 @@ class HotPath:
                 raise ValueError(f"dout must be [{self.B}][{self.width}] {self.ts.dtype}")
 
     def forward(self, x, idx):
+        if self.step_api:
+            self.step_fwd(x, idx)
+            return self.out
         if self.overlap_indexer:
             main = torch.cuda.current_stream(self.ts.device)
             self._side.wait_stream(main)
@@ -154,6 +180,9 @@ class HotPath:
         return self.out
 
     def backward(self, idx, dout):
+        if self.step_api:
+            self.step_bwd(dout, idx=idx)
+            return self.dx
         # without ys (and deterministic), the indexer is built inside the backward's launch
         in_bwd = not self.materialize_ys and self.indexer is not None and not self.overlap_indexer
         self.interact_bwd(dout, idx=idx, build_indexer=in_bwd)

@@ -148,7 +148,7 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
  * so the step's dlrm_sgd_update can pass DLRM_UPDATE_PREBUILT.
  * Declared after the indexer type below; see the SparseIndexer section. */
 
-/* ---- sparse indexer + SGD scatter update/* ---- sparse indexer + SGD scatter update --------------------------------------------- */
+/* ---- sparse indexer + SGD scatter update --------------------------------------------- */
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_table,
                         dlrm_indexer** out);
 int dlrm_indexer_destroy(dlrm_indexer* indexer);
@@ -182,6 +182,34 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer, u
                     int batch, int lookups,
                     const void* grad, int grad_dtype, int64_t grad_ld, int64_t grad_offset,
                     float lr);
+
+/* ---- training step: fused forms of the four operators --------------------------------
+ * One train! iteration of the sparse half of the model (src/train/train.jl:215-227 and
+ * custom_update! :283-290) on one-hot lookups, as two launching calls with the tables
+ * unchanged between them:
+ *
+ * dlrm_step_fwd = dlrm_lookup_interact_fwd(ys = NULL) + dlrm_indexer_build, in one launch
+ *   where the shape allows (F <= 32, batch <= 2048): the indexer's workgroups sort while the
+ *   gather streams.  `out` is bit-identical to dlrm_lookup_interact_fwd's.  The indexer is
+ *   built in "split" form: rows hit by exactly one position of the batch are flagged for the
+ *   backward instead of listed for the apply (dlrm_sgd_update refuses such an indexer).
+ * dlrm_step_bwd = dlrm_interact_bwd_gather + dlrm_sgd_update(Descent(lr), PREBUILT) with that
+ *   indexer.  dx is bit-identical to dlrm_interact_bwd_gather's and the tables end up
+ *   bit-identical to dlrm_sgd_update's result: a once-hit row gets w = fmaf(-lr, g, w) inside
+ *   the backward (no other sample reads it), so its dt row is never written or read back;
+ *   dt holds only the rows the apply launch reads (x rows and rows of repeated table rows).
+ *   dx and dt must be 16-B aligned with leading dimensions divisible by 4.
+ *   flags: 0 runs both launches; DLRM_STEP_BWD_ONLY then DLRM_STEP_APPLY_ONLY run them one at a
+ *   time (e.g. the apply on another stream, or timed alone). */
+#define DLRM_STEP_BWD_ONLY 1u   /* the backward launch only (dx, dt, once-hit rows)       */
+#define DLRM_STEP_APPLY_ONLY 2u /* the apply of repeated rows only (reads dt)             */
+int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tables, dlrm_indexer* indexer,
+                  const void* indices, int itype, int64_t table_stride, int index_base, int batch,
+                  const void* x, int64_t x_ld, void* out, int64_t out_ld, int padding);
+int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
+                  const void* indices, int itype, int64_t table_stride, int index_base, int batch,
+                  const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,
+                  float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr, unsigned flags);
 
 #ifdef __cplusplus
 }

@@ -361,8 +361,109 @@ def test_hotpath_step_matches_operator_sequence(pkg, gpu, overlap, materialize):
     pkg.update_(pkg.Descent(0.25), ts2, pkg.maplookup_pullback(D, ts2, p, dy), index_base=0)
     assert np.array_equal(to_np_f32(hp.out), to_np_f32(out))
     assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
-    assert np.array_equal(to_np_f32(hp.dt), to_np_f32(dy))
+    m = _dt_written_mask(idx.cpu().numpy(), D) if hp.step_api else slice(None)
+    assert np.array_equal(to_np_f32(hp.dt)[m], to_np_f32(dy)[m])
     for a, b in zip(hp.ts, ts2):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+
+
+def _dt_written_mask(idx, D):
+    """[B][F*D] bool: the dt entries dlrm_step_bwd must write -- the x rows and the rows of
+    positions whose table row is hit more than once (once-hit rows are updated in place)."""
+    T, B = idx.shape
+    keep = np.ones((B, T + 1), dtype=bool)
+    for t in range(T):
+        _, inv, cnt = np.unique(idx[t], return_inverse=True, return_counts=True)
+        keep[:, t + 1] = cnt[inv] > 1
+    return np.repeat(keep, D, axis=1)
+
+
+@pytest.mark.parametrize("rows,D,B,zipf,dtype", [
+    ([10, 3000, 7, 100000], 32, 512, None, torch.float32),            # F = 5: one 16-row block
+    ("kaggle", 16, 2048, None, torch.float32),                         # F = 27, N = 2048: split form
+    ([3, 4, 10, 1000, 5_000_000], 128, 2048, 1.1, torch.float32),      # hot rows (multi-slice segments)
+    ([5, 100000, 3, 77] * 6 + [9, 10], 128, 300, None, torch.bfloat16),
+    ([300, 100000, 5_000_000], 64, 3000, None, torch.float32),         # N > 2048: unsplit fallback
+    ([50] * 40, 32, 200, None, torch.float32),                         # F = 41: unsplit fallback
+    ([1], 16, 64, None, torch.float32)])                               # every position hits one row
+def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
+    """dlrm_step_fwd / dlrm_step_bwd (indexer built in the forward's launch, once-hit rows
+    updated inside the backward) == maplookup -> DotInteraction -> dot_back -> update!
+    bit for bit: out, dx, the updated tables, and every dt row the apply reads."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    rng = np.random.default_rng(B + D)
+    T = len(rows)
+    idx_np = rand_indices(rng, rows, B, 1, zipf=zipf)
+    tabs = [rng.uniform(-1, 1, size=(n, D)).astype(np.float32) for n in rows]
+    idx = torch.from_numpy(idx_np).to(torch.int32).to(gpu)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu).to(dtype)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0)
+    assert hp.step_api
+    p = pkg.PackedIndices(idx)
+    for _ in range(2):  # two steps: the second reads rows the first updated
+        hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    ts2 = pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype))
+    for _ in range(2):
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts2, p, index_base=0)
+        out, back = pkg.rrule(pkg.DotInteraction(), x, ys)
+        _, dx, dy = back(dout)
+        pkg.update_(pkg.Descent(0.5), ts2, pkg.maplookup_pullback(D, ts2, p, dy), index_base=0)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_bits(hp.out), to_np_bits(out))
+    assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
+    m = _dt_written_mask(idx_np, D)
+    assert np.array_equal(to_np_f32(hp.dt)[m], to_np_f32(dy)[m])
+    for a, b in zip(hp.ts, ts2):
+        assert np.array_equal(to_np_bits(a.data), to_np_bits(b.data))
+
+
+def test_step_api_state_and_bounds(pkg, gpu):
+    """A split indexer is refused by the plain update; step_bwd needs step_fwd's indices; an
+    out-of-range index raises BoundsError and the step still matches the operator sequence on
+    the valid positions."""
+    rows, D, B = [100, 7, 5000], 16, 256
+    rng = np.random.default_rng(3)
+    tabs = rand_tables(rng, rows, D)
+    idx_np = rand_indices(rng, rows, B, 1)
+    idx = torch.from_numpy(idx_np).to(torch.int32).to(gpu)
+    x = torch.randn((B, D), device=gpu)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=1.0, index_base=0)
+    dout = torch.randn((B, hp.width), device=gpu)
+    p = pkg.PackedIndices(idx)
+    hp.step_fwd(x, p)
+    with pytest.raises(pkg.DLRMError) as e:
+        hp.sgd_update(p, prebuilt=True)
+    assert e.value.code == pkg._lib.E_STATE
+    other = pkg.PackedIndices(idx.clone())
+    with pytest.raises(pkg.DLRMError) as e:
+        hp.step_bwd(dout, x=x, idx=other)
+    assert e.value.code == pkg._lib.E_STATE
+    hp.step_bwd(dout, x=x, idx=p)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    # out-of-range: skipped everywhere, flagged once
+    bad_np = idx_np.copy()
+    bad_np[1, 5] = rows[1] + 3
+    bad = pkg.PackedIndices(torch.from_numpy(bad_np).to(torch.int32).to(gpu))
+    hp2 = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=1.0, index_base=0)
+    hp2.step(x, bad, dout)
+    with pytest.raises(pkg.BoundsError):
+        hp2.check_bounds()
+    ts2 = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts2, bad, index_base=0, check_bounds=False)
+    out, back = pkg.rrule(pkg.DotInteraction(), x, ys)
+    _, dx, dy = back(dout)
+    pkg.update_(pkg.Descent(1.0), ts2, pkg.maplookup_pullback(D, ts2, bad, dy), index_base=0, check_bounds=False)
+    with pytest.raises(pkg.BoundsError):  # the operators flagged it too (and this clears the flag)
+        ts2.ctx.check_bounds()
+    assert np.array_equal(to_np_f32(hp2.out), to_np_f32(out))
+    assert np.array_equal(to_np_f32(hp2.dx), to_np_f32(dx))
+    for a, b in zip(hp2.ts, ts2):
         assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
 
 

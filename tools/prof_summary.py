@@ -19,11 +19,11 @@ import re
 from collections import defaultdict
 
 STAGES = [  # (regex on the kernel name, stage)
-    (r"interact_fwd_kernel<[^,]+, \d+, true>", "lookup_interact_fwd"),
-    (r"interact_fwd_kernel<[^,]+, \d+, false>|interact_fwd_scalar", "interact_fwd"),
+    (r"interact_fwd_kernel<[^,]+, \d+, true(, \d+)?>", "lookup_interact_fwd"),
+    (r"interact_fwd_kernel<[^,]+, \d+, false(, \d+)?>|interact_fwd_scalar", "interact_fwd"),
     (r"interact_bwd", "interact_bwd"),  # incl. interact_bwd_index_kernel
     (r"maplookup_", "lookup"),
-    (r"indexer_build_kernel", "indexer_build"),
+    (r"indexer_build_kernel|indexer_fast_kernel", "indexer_build"),
     (r"sgd_apply|sgd_chunks", "sgd_update"),
     (r"sgd_hot", "sgd_update"),
     (r"sgd_atomic", "sgd_update"),
