@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_HERE, "lib", "libdlrm_hip.so")
+LIB_PATH = os.environ.get("DLRM_HIP_LIB") or os.path.join(_HERE, "lib", "libdlrm_hip.so")  # override: A/B runs
 HEADER = os.path.join(REPO, "include", "dlrm_hip.h")
 
 # dlrm_status

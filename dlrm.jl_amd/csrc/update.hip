@@ -23,6 +23,8 @@
 // bitwise reproducible, and no inter-workgroup hand-off.  DLRM_UPDATE_ATOMIC instead adds
 // -lr*g straight into the table with global_atomic_add_f32 (no sort, non-deterministic
 // rounding order).
+#include <cstdlib>
+
 #include "common.hpp"
 
 #ifdef DLRM_PHASE
@@ -694,13 +696,12 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     if (T_ == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
-#ifdef DLRM_PHASE
-    if (getenv("DLRM_IX256") && N <= 2048) {  // profiling: the 256-thread form the backward launch uses
+    static const bool ix256 = getenv("DLRM_IX256") != nullptr;  // experiment knob
+    if (ix256 && N <= 2048) {  // the 256-thread form the forward / backward launches use, on its own
         hipLaunchKernelGGL((indexer_fast_kernel<256, 8>), dim3(T_), dim3(256), sizeof(FastLds<256, 8>), s, ix, tabs,
                            idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
         return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
     }
-#endif
     if (N <= 1024 * 2) {
         hipLaunchKernelGGL((indexer_fast_kernel<1024, 2>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 2>), s, ix, tabs,
                            idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
