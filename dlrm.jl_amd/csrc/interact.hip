@@ -110,10 +110,11 @@ struct GatherArgs {
 };
 
 // Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
-template <typename T, int NB, bool FUSED, int WPB, bool POOL = false>
-__device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all, int d, int F, int B,
+template <typename T, int NB, bool FUSED, int WPB, bool POOL = false, int DC = 0>
+__device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all, int d_, int F, int B,
                                          const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                          T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga) {
+    const int d = DC > 0 ? DC : d_;  // DC: the feature size as a compile-time constant
     typedef Frag<T> FR;
     typedef typename FR::type frag;
     constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
@@ -251,13 +252,13 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
 }
 
 // POOL: the pooled-bag path (lookups > 1) is compiled in; the one-hot kernel stays lean.
-template <typename T, int NB, bool FUSED, bool POOL, int WPB = 4>
+template <typename T, int NB, bool FUSED, bool POOL, int DC = 0, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                    int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                                                    T* __restrict__ out, int64_t out_ld, int padding,
                                                                    GatherArgs ga) {
     __shared__ float stage_all[WPB * kStage];
-    fwd_body<T, NB, FUSED, WPB, POOL>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding,
+    fwd_body<T, NB, FUSED, WPB, POOL, DC>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding,
                                 ga);
 }
 
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F,
 // lookup + interaction without ys.  The indexer depends only on the indices, so it streams
 // beside the gather instead of adding a launch.
 constexpr int kStepIndexEPL = 8;  // positions per thread: N <= 2048
-template <typename T, int NB>
+template <typename T, int NB, int DC = 0>
 __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                  int64_t x_ld, T* __restrict__ out, int64_t out_ld,
                                                                  int padding, GatherArgs ga, IndexerDev ix) {
@@ -279,8 +280,8 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
                                                    ga.itype, ga.tstride, ga.base, B * ga.L, ga.err, sl);
         return;
     }
-    fwd_body<T, NB, true, 4>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, x, x_ld, nullptr, 0, out, out_ld, padding,
-                             ga);
+    fwd_body<T, NB, true, 4, false, DC>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, x, x_ld, nullptr, 0, out,
+                                        out_ld, padding, ga);
 }
 
 // ---------------------------------------------------------------------------------- bwd
@@ -318,12 +319,13 @@ struct StepUpdate {
     float lr;
 };
 
-template <typename T, int NB, bool GATHER, bool UPD = false, int SBU_ = 0>
-__device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int d, int F, int B,
+template <typename T, int NB, bool GATHER, bool UPD = false, int SBU_ = 0, int DC = 0>
+__device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int d_, int F, int B,
                                          const T* __restrict__ dout, int64_t dout_ld, const T* __restrict__ t,
                                          int64_t t_ld, float* __restrict__ dx, int64_t dx_ld,
                                          float* __restrict__ dt, int64_t dt_ld, const GatherArgs& ga,
                                          const T* __restrict__ x, int64_t x_ld, const StepUpdate& su = StepUpdate{}) {
+    const int d = DC > 0 ? DC : d_;  // DC: the feature size as a compile-time constant
     typedef BwdGeom<NB> G;
     constexpr int KS = 4 * NB;          // max k-steps (F <= 16 NB)
     constexpr int SBU = SBU_ > 0 ? SBU_ : (NB <= 2 ? 2 : 1);  // 64-column super-blocks loaded together
@@ -368,7 +370,7 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
                 rowp[s] = (s < ksteps && kk == 0) ? x + b * x_ld : (ok ? (const T*)td.data + r * d : nullptr);
             }
         }
-        T* urow[NB][4];  // UPD: the once-hit table row of output row f = 16I + 4q + r, else null
+        uint32_t urow[NB][4];  // UPD: the once-hit table row of output row f = 16I + 4q + r, else ~0u
         if (UPD) {
             uint8_t fl[NB][4];
             int64_t ui[NB][4];
@@ -389,8 +391,7 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
                     const bool tab = f >= 1 && f < F;
                     const TableDesc td = tds[tab ? f - 1 : 0];
                     const int64_t rr = ui[I][r] - ga.base;
-                    urow[I][r] = (tab & (fl[I][r] != 0) & (rr >= 0) & (rr < td.nrows)) ? (T*)td.data + rr * d
-                                                                                       : nullptr;
+                    urow[I][r] = (tab & (fl[I][r] != 0) & (rr >= 0) & (rr < td.nrows)) ? (uint32_t)rr : ~0u;
                 }
         }
         // The first super-blocks' T rows (and dout's x part) go out before S is built, so their
@@ -494,12 +495,12 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
                             const int f = I * 16 + 4 * q + r;
                             if (f < F) {
                                 const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
-                                if (UPD && urow[I][r]) {
+                                if (UPD && urow[I][r] != ~0u) {
                                     const f32x4_t tw = *(const f32x4_t*)(Tt + f * 64 + 4 * c);
                                     float wv[4];
 #pragma unroll
                                     for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
-                                    store_row<T, 4>(urow[I][r], n0, wv);
+                                    store_row<T, 4>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
                                 } else {
                                     stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
                                 }
@@ -552,15 +553,15 @@ __global__ __launch_bounds__(256, 3) void interact_bwd_index_kernel(int d, int F
 // The backward of a training step after interact_fwd_index_kernel: re-gathers T, writes dx
 // and the dt rows of positions whose row is hit more than once, and applies the SGD step to
 // once-hit rows itself (the apply launch that follows handles the rest).
-template <typename T, int NB, int SBU>
+template <typename T, int NB, int SBU, int DC = 0>
 __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int F, int B, const T* __restrict__ dout,
                                                                   int64_t dout_ld, float* __restrict__ dx,
                                                                   int64_t dx_ld, float* __restrict__ dt, int64_t dt_ld,
                                                                   GatherArgs ga, const T* __restrict__ x, int64_t x_ld,
                                                                   StepUpdate su) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    bwd_body<T, NB, true, true, SBU>(blockIdx.x, gridDim.x, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
-                                     dt_ld, ga, x, x_ld, su);
+    bwd_body<T, NB, true, true, SBU, DC>(blockIdx.x, gridDim.x, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld,
+                                         dt, dt_ld, ga, x, x_ld, su);
 }
 
 // ------------------------------------------------------------------ scalar fallbacks
@@ -645,6 +646,9 @@ static void launch_fwd_nb(hipStream_t s, int cus, int d, int F, int B, const voi
     if (FUSED && ga.L > 1)
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, true>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
                            x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+    else if (d == 128)  // the BASELINE feature size, compiled for it
+        hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, false, 128>), dim3(g), dim3(256), 0, s, d, F, B,
+                           (const T*)x, x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
     else
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, false>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
                            x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
@@ -836,8 +840,12 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
     if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
     const unsigned g = grid_for(B, 4, cus) + T_;
 #define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
-    hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_>), dim3(g), dim3(256), lds, s, d, F, B, (const TY*)x, x_ld, \
-                       (TY*)out, out_ld, padding, ga, ix);
+    if (d == 128)                                                                                                  \
+        hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_, 128>), dim3(g), dim3(256), lds, s, d, F, B,            \
+                           (const TY*)x, x_ld, (TY*)out, out_ld, padding, ga, ix);                                   \
+    else                                                                                                           \
+        hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_>), dim3(g), dim3(256), lds, s, d, F, B, (const TY*)x,   \
+                           x_ld, (TY*)out, out_ld, padding, ga, ix);
     if (dtype == DLRM_F32) {
         if (NB == 1) DLRM_LAUNCH_FWDIX(float, 1) else DLRM_LAUNCH_FWDIX(float, 2)
     } else {
@@ -867,14 +875,16 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     {                                                                                                              \
         typedef BwdGeom<N_> G;                                                                                     \
         const size_t lds = sizeof(float) * G::template lds_floats<true>() * G::WPB + sizeof(TableDesc) * T_;       \
-        if (sbu == 2)                                                                                              \
-            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 2>), dim3(grid_for(B, G::WPB, cus)),             \
-                               dim3(64 * G::WPB), lds, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, \
-                               (const TY*)x, x_ld, su);                                                            \
+        const dim3 grid(grid_for(B, G::WPB, cus)), blk(64 * G::WPB);                                               \
+        if (d == 128 && sbu == 2)                                                                                  \
+            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 2, 128>), grid, blk, lds, s, d, F, B,             \
+                               (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x, x_ld, su);         \
+        else if (d == 128)                                                                                         \
+            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 1, 128>), grid, blk, lds, s, d, F, B,             \
+                               (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x, x_ld, su);         \
         else                                                                                                       \
-            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 1>), dim3(grid_for(B, G::WPB, cus)),             \
-                               dim3(64 * G::WPB), lds, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, \
-                               (const TY*)x, x_ld, su);                                                            \
+            hipLaunchKernelGGL((interact_bwd_update_kernel<TY, N_, 1>), grid, blk, lds, s, d, F, B, (const TY*)dout, \
+                               dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x, x_ld, su);                          \
     }
     if (dtype == DLRM_F32) {
         if (NB == 1) DLRM_LAUNCH_BWDUP(float, 1) else DLRM_LAUNCH_BWDUP(float, 2)
