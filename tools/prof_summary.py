@@ -19,7 +19,7 @@ import re
 from collections import defaultdict
 
 STAGES = [  # (regex on the kernel name, stage)
-    (r"interact_fwd_kernel<[^,]+, \d+, true(, \d+)?>", "lookup_interact_fwd"),
+    (r"interact_fwd_kernel<[^,]+, \d+, true(, \d+)?>|interact_fwd_index_kernel", "lookup_interact_fwd"),
     (r"interact_fwd_kernel<[^,]+, \d+, false(, \d+)?>|interact_fwd_scalar", "interact_fwd"),
     (r"interact_bwd", "interact_bwd"),  # incl. interact_bwd_index_kernel
     (r"maplookup_", "lookup"),
