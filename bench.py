@@ -64,7 +64,9 @@ def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks, materialize_ys=True):
         "interact_fwd": B * (d * E + (F - 1) * D * E + d * E + (d + P) * E),
         "interact_bwd": B * ((d + P) * E + t_r + F * D * 4 + d * 4),
         "indexer_build": T * N * I + T * N * 4 + uniq * 8 + chunks * 16,
-        "sgd_update": T * N * (4 + D * 4) + uniq * 2 * D * E + chunks * 16,
+        # positions (perm) + each bag's gradient row once (pooled: shared by its L lookups) +
+        # read-modify-write of every touched row + the chunk descriptors
+        "sgd_update": T * N * 4 + T * B * D * 4 + uniq * 2 * D * E + chunks * 16,
     }
 
 
@@ -109,11 +111,28 @@ def make_inputs(pkg, w, B, dev, rank, T_rows):
         t = torch.empty((n, D), dtype=torch.float32, device=dev).uniform_(-s, s, generator=g)
         tables.append(t.to(dt) if dt != torch.float32 else t)
     idx = []
+    zipf = w.get("zipf")
+    rng = np.random.default_rng(51234 + rank)
     for _ in range(NBATCH):
+        if zipf:
+            cols = [torch.from_numpy(zipf_rows(rng, n, B * L, zipf)) for n in T_rows]
+            idx.append(torch.stack(cols).to(dev).contiguous())
+            continue
         cols = [torch.randint(0, n, (B * L,), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
                 for n in T_rows]
         idx.append(torch.stack(cols).contiguous())
     return tables, idx, g
+
+
+def zipf_rows(rng, n, size, s):
+    """Zipf(s) ranks (rank 0 hottest, tail folded mod n) scattered over the table's rows by an
+    affine bijection r -> (a*r + c) mod n, so hot rows sit at random places."""
+    z = (rng.zipf(s, size=size) - 1) % n
+    a = int(rng.integers(1, max(n, 2)))
+    while np.gcd(a, n) != 1:
+        a += 1
+    c = int(rng.integers(0, n))
+    return ((z.astype(np.int64) * a + c) % n).astype(np.int32)
 
 
 def cpu_baseline(pkg, w, seconds, threads):
@@ -132,7 +151,10 @@ def cpu_baseline(pkg, w, seconds, threads):
         a = np.empty((n, D), dtype=np.float32)
         oracle.fill_uniform(a, -1.0 / np.sqrt(n), 1.0 / np.sqrt(n), 1000 + t, threads)
         tables.append(a)
-    batches = [np.stack([rng.integers(0, n, size=B * L) for n in rows]).astype(np.int64) for _ in range(4)]
+    if w.get("zipf"):
+        batches = [np.stack([zipf_rows(rng, n, B * L, w["zipf"]) for n in rows]).astype(np.int64) for _ in range(4)]
+    else:
+        batches = [np.stack([rng.integers(0, n, size=B * L) for n in rows]).astype(np.int64) for _ in range(4)]
     x = rng.standard_normal((B, D)).astype(np.float32)
     dout = (rng.standard_normal((B, D + P)) * 1e-3).astype(np.float32)
     ys = np.zeros((B, F * D), dtype=np.float32)

@@ -342,6 +342,10 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
     ix->dev.pdim = kPartialDim;
+    const int64_t hs = cap > kFastMaxN ? hix_table_slots(cap) : 0;
+    ix->dev.hsize = hs;
+    ix->dev.hbits = 0;
+    while (((int64_t)1 << ix->dev.hbits) < hs) ++ix->dev.hbits;
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
     const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1));
@@ -352,6 +356,10 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.hot_slice, n * 4}, {(void**)&ix->dev.hot_cnt, n * 4},
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n},
+        // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
+        {(void**)&ix->dev.pslot, hs ? n * 4 : 0},    {(void**)&ix->dev.hkey, (size_t)(T * hs) * 4},
+        {(void**)&ix->dev.hcnt, (size_t)(T * hs) * 4}, {(void**)&ix->dev.hseg, (size_t)(T * hs) * 8},
+        {(void**)&ix->dev.hfill, (size_t)(T * hs) * 4}, {(void**)&ix->dev.hstate, hs ? (size_t)T * 32 : 0},
     };
     size_t total = 0;
     for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
@@ -365,8 +373,16 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     }
     char* base = (char*)ix->block;
     for (auto& pc : pieces) {
-        *pc.p = base;
+        *pc.p = pc.bytes ? base : nullptr;
         base += (pc.bytes + 255) & ~(size_t)255;
+    }
+    if (hs) {  // every slot starts empty (the alloc pass resets the slots it used)
+        rc = ctx_hip(ctx, hipMemset(ix->dev.hkey, 0xff, (size_t)(T * hs) * 4), "hipMemset(hash keys)");
+        if (rc != DLRM_OK) {
+            (void)hipFree(ix->block);
+            delete ix;
+            return rc;
+        }
     }
     *out = ix;
     return DLRM_OK;
@@ -506,6 +522,13 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
                         "dlrm_step_fwd: no fused forward for this shape (16-B aligned rows and x, F <= 96 needed)");
     if (rc) return rc;
+    if (ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
+        // large batch: the hash build in its split form (once-hit rows left to dlrm_step_bwd)
+        rc = launch_hix_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, true);
+        if (rc) return rc;
+        record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+        return DLRM_OK;
+    }
     return dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, 1);
 }
 

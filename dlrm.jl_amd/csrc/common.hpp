@@ -140,6 +140,9 @@ __device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
 
 namespace dlrm {
 // Per-table indexer arrays (device), each [T][cap] (seg_start [T][cap+1]).
+constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions per table
+constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
+
 struct IndexerDev {
     uint32_t* keys0;  uint32_t* keys1;   // global sort scratch (cap > kLdsSortMax)
     int32_t* vals0;   int32_t* vals1;
@@ -153,6 +156,15 @@ struct IndexerDev {
     float* partial;        // [T][pcap][pdim] slice partial sums (multi-slice hot segments)
     int32_t* counts;       // [T][8]: U, chunks, hot, slices, nvalid
     uint8_t* single;       // [T][cap]: 1 = the position's row is hit once in the batch (split builds)
+    // hash indexer (hashindex.hip; capacities above the in-LDS build's kFastMaxN)
+    int32_t* pslot;        // [T][cap] hash slot of each position (-1: invalid index)
+    uint32_t* hkey;        // [T][hsize] row of each slot, 0xffffffff = empty (reset by the alloc pass)
+    uint32_t* hcnt;        // [T][hsize] positions per slot (reset by the alloc pass)
+    int2* hseg;            // [T][hsize] {first perm entry, length} of the slot's segment
+    uint32_t* hfill;       // [T][hsize] placement cursor
+    unsigned long long* hstate;  // [T][4] {segments << 32 | positions} allocation cursor, ...
+    int64_t hsize;         // slots per table (power of two >= 2 cap), 0 = no hash arrays
+    int hbits;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)
     int pdim;              // partial row capacity (elements)
@@ -193,6 +205,9 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T, int dtype, cons
                     float lr);
 int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
+int64_t hix_table_slots(int64_t cap);
+int launch_hix_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
+                     int64_t tstride, int base, int N, bool split);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
                          int itype, int64_t tstride, int base, int B, int L);
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,

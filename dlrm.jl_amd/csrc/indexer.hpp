@@ -59,7 +59,6 @@ __device__ __forceinline__ V block_scan_nw(V v, V* wtot, V* tot) {
 //    skewed rows take the remaining LSD passes.
 //  * Segments and the chunk / hot lists: one head-flag scan and one packed 64-bit scan.
 // Output format = indexer_build_kernel's (the apply kernel and dlrm_indexer_read unchanged).
-constexpr int kFastMaxN = 4096;
 
 // NT threads (1024 standalone; 256 inside the backward launch), EPL positions per thread.
 // Digit width: 8 bits with 16 waves, 11 bits with 4 (about one key per bucket at N = 2048, so
@@ -395,5 +394,74 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
     }
     PHASE(22);
 }
+
+// ------------------------------------------------- flat (table, item) lookup over counts
+// Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
+// may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb, int key, int& table, int& local) {
+    // count of lanes with incl <= key (binary lifting over the non-decreasing prefix)
+    int pos = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const int vv = __shfl(incl, pos + step - 1, 64);
+        if (vv <= key) pos += step;
+    }
+    const int before = __shfl(incl, pos > 0 ? pos - 1 : 0, 64);
+    if (table < 0 && key >= 0 && key < tile_total) {
+        table = tb + pos;
+        local = key - (pos > 0 ? before : 0);
+    }
+}
+
+// Per-wave prefix of one count over the tables (T <= 64 kept in registers; more tables are
+// re-scanned tile by tile on every lookup).
+struct TableScan {
+    int incl;   // this lane's inclusive prefix (tile 0)
+    int total;  // over all tables
+};
+
+__device__ __forceinline__ TableScan scan_counts(const IndexerDev& ix, int T_, int which) {
+    const int lane = threadIdx.x & 63;
+    TableScan r{0, 0};
+    for (int tb = 0; tb < T_; tb += 64) {
+        const int tt = tb + lane;
+        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
+        const int incl = wave_incl_scan(c);
+        if (tb == 0) r.incl = incl;
+        r.total += __shfl(incl, 63, 64);
+    }
+    return r;
+}
+
+__device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, const TableScan& sc, int id,
+                                       int& table, int& local) {
+    table = -1;
+    local = 0;
+    if (T_ <= 64) {
+        locate_in_tile(sc.incl, sc.total, 0, id, table, local);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    int run = 0;
+    for (int tb = 0; tb < T_; tb += 64) {
+        const int tt = tb + lane;
+        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
+        const int incl = wave_incl_scan(c);
+        const int tot = __shfl(incl, 63, 64);
+        locate_in_tile(incl, tot, tb, id - run, table, local);
+        run += tot;
+    }
+}
+
 
 }  // namespace dlrm

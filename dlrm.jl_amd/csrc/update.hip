@@ -414,73 +414,6 @@ __device__ __forceinline__ void sum_staged(const int32_t* stage, int m, int L, c
     }
 }
 
-// Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
-// may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.
-__device__ __forceinline__ int wave_incl_scan(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    return x;
-}
-
-__device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb, int key, int& table, int& local) {
-    // count of lanes with incl <= key (binary lifting over the non-decreasing prefix)
-    int pos = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-        const int vv = __shfl(incl, pos + step - 1, 64);
-        if (vv <= key) pos += step;
-    }
-    const int before = __shfl(incl, pos > 0 ? pos - 1 : 0, 64);
-    if (table < 0 && key >= 0 && key < tile_total) {
-        table = tb + pos;
-        local = key - (pos > 0 ? before : 0);
-    }
-}
-
-// Per-wave prefix of one count over the tables (T <= 64 kept in registers; more tables are
-// re-scanned tile by tile on every lookup).
-struct TableScan {
-    int incl;   // this lane's inclusive prefix (tile 0)
-    int total;  // over all tables
-};
-
-__device__ __forceinline__ TableScan scan_counts(const IndexerDev& ix, int T_, int which) {
-    const int lane = threadIdx.x & 63;
-    TableScan r{0, 0};
-    for (int tb = 0; tb < T_; tb += 64) {
-        const int tt = tb + lane;
-        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
-        const int incl = wave_incl_scan(c);
-        if (tb == 0) r.incl = incl;
-        r.total += __shfl(incl, 63, 64);
-    }
-    return r;
-}
-
-__device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, const TableScan& sc, int id,
-                                       int& table, int& local) {
-    table = -1;
-    local = 0;
-    if (T_ <= 64) {
-        locate_in_tile(sc.incl, sc.total, 0, id, table, local);
-        return;
-    }
-    const int lane = threadIdx.x & 63;
-    int run = 0;
-    for (int tb = 0; tb < T_; tb += 64) {
-        const int tt = tb + lane;
-        const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
-        const int incl = wave_incl_scan(c);
-        const int tot = __shfl(incl, 63, 64);
-        locate_in_tile(incl, tot, tb, id - run, table, local);
-        run += tot;
-    }
-}
-
 // Cross-workgroup hand-off of slice partials (cdna_hip_programming.md Guideline 16, R1):
 // payload stored write-through (sc1, agent-scope atomic stores), every storing wave drains
 // (vmcnt(0)) before the workgroup barrier, ONE lane adds to the segment's arrival counter;
@@ -712,6 +645,8 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
         (void)a4;
         hipLaunchKernelGGL((indexer_fast_kernel<1024, 4>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 4>), s, ix, tabs, idx,
                            itype, tstride, base, (int)N, ctx_error_word(ctx));
+    } else if (ix.hsize && N <= kHixMaxN) {
+        return launch_hix_build(ctx, ix, tabs, T_, idx, itype, tstride, base, (int)N, false);
     } else
         hipLaunchKernelGGL(indexer_build_kernel<false>, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, idx, itype,
                            tstride, base, B, L, ctx_error_word(ctx));

@@ -206,7 +206,13 @@ def _np_segments(idx_row):
 @pytest.mark.parametrize("rows,B,L,zipf", [([3, 4, 10, 1000, 5_000_000], 2048, 1, None), ([1000, 7, 20000], 300, 10, None),
                                            ([2], 1, 1, None), ([100000, 3], 5000, 1, None), ([256, 257, 70000], 2048, 1, None),
                                            ([300, 100000, 5_000_000], 2048, 1, 1.1), ([100000, 1000], 4000, 2, 1.2),
-                                           ([0x10000, 0x1000000], 1500, 1, None)])
+                                           ([0x10000, 0x1000000], 1500, 1, None),
+                                           # hash build (N > 4096): all-distinct, tiny, skewed, pooled
+                                           ([3, 4, 10, 1000, 5_000_000], 8192, 1, None),
+                                           ([1_000_000, 1_000_000, 3], 2048, 10, 1.2),
+                                           ([2, 100000, 33_000_000], 16384, 1, None),
+                                           ([5000], 4097, 1, 1.05), ([1], 6000, 1, None),
+                                           ([64] * 3, 300, 20, None)])
 def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
     """Both sort strategies (1 pass + bucket rank; full LSD radix on skewed rows), LDS and
     global-scratch variants: unique rows and per-row positions must match numpy exactly."""
@@ -219,15 +225,19 @@ def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
 
 
 def _assert_segments(ix, idx, N):
+    """One segment per distinct row (segment order unspecified), holding exactly that row's
+    positions in ascending order (vectorised: large-N builds have ~N segments per table)."""
     for t in range(idx.shape[0]):
-        urows, _ = _np_segments(idx[t])
         got_rows, pos, seg = ix.segments(t)
-        assert sorted(got_rows) == urows.tolist()  # one segment per distinct row (segment order unspecified)
-        assert seg[-1] == N and len(seg) == len(urows) + 1
-        for s_, r in enumerate(got_rows):
-            members = pos[seg[s_]:seg[s_ + 1]]
-            want = np.flatnonzero(idx[t] == r).tolist()
-            assert members == want  # exactly this row's positions, ascending
+        got_rows, pos, seg = np.asarray(got_rows, dtype=np.int64), np.asarray(pos), np.asarray(seg)
+        order = np.argsort(idx[t], kind="stable")
+        urows, starts, counts = np.unique(idx[t][order], return_index=True, return_counts=True)
+        assert len(got_rows) == len(urows) and seg[-1] == N and len(seg) == len(urows) + 1
+        assert np.array_equal(np.sort(got_rows), urows)
+        k = np.searchsorted(urows, got_rows)
+        assert np.array_equal(np.diff(seg), counts[k])
+        want = order[np.repeat(starts[k] - seg[:-1], counts[k]) + np.arange(N)]
+        assert np.array_equal(pos, want)
 
 
 @pytest.mark.parametrize("rows,B,zipf", [([3, 4, 10, 1000, 5_000_000], 2048, None), ([300, 100000, 5_000_000], 2048, 1.1),
@@ -285,6 +295,56 @@ def test_sgd_update_vs_oracle(pkg, gpu, dim, L):
         assert_close(new[touched], ref[t][touched], rtol=1e-6, scale=scale, what=f"table {t}")
         untouched = np.setdiff1d(np.arange(rows[t]), touched)
         assert np.array_equal(new[untouched], tabs[t][untouched])
+
+
+@pytest.mark.parametrize("rows,B,L,zipf", [([3, 1000, 1_000_000], 2048, 10, 1.2), ([7, 200000], 8192, 1, None)])
+def test_sgd_update_hash_build_vs_oracle(pkg, gpu, rows, B, L, zipf):
+    """update! with B*L > 4096 positions per table (the hash-built indexer) against the oracle."""
+    rng = np.random.default_rng(B * L)
+    D, Pd = 64, 8
+    tabs = rand_tables(rng, rows, D)
+    idx = rand_indices(rng, rows, B, L, zipf=zipf)
+    grad = rng.standard_normal((B, Pd + D * len(rows))).astype(np.float32)
+    ref = [t.copy() for t in tabs]
+    uniq = oracle.sgd_update(ref, idx, 0, B, L, grad, Pd, 0.25)
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    pidx = pkg.PackedIndices(torch.from_numpy(idx).reshape(len(rows), B, L).to(gpu))
+    ix = pkg.SparseIndexer(len(rows), B * L, gpu)
+    pkg.update_(pkg.Descent(0.25), ts, pkg.maplookup_pullback(Pd, ts, pidx, torch.from_numpy(grad).to(gpu)), ix,
+                index_base=0)
+    torch.cuda.synchronize()
+    for t in range(len(rows)):
+        assert len(ix.unique_rows(t)) == uniq[t]
+        new = to_np_f32(ts[t].data)
+        touched = np.unique(idx[t])
+        assert_close(new[touched], ref[t][touched], rtol=1e-6, scale=0.25 * np.abs(grad).max() * B * L,
+                     what=f"table {t}")
+        untouched = np.setdiff1d(np.arange(rows[t]), touched)
+        assert np.array_equal(new[untouched], tabs[t][untouched])
+
+
+def test_hash_build_bounds_error_and_reuse(pkg, gpu):
+    """Large-N build: an out-of-range index is skipped and flagged; the next build with the
+    same indexer (slots reset by the previous build) is exact again."""
+    rows, B = [10, 50000], 6000
+    rng = np.random.default_rng(11)
+    idx = rand_indices(rng, rows, B, 1)
+    bad = idx.copy()
+    bad[1, 17] = rows[1] + 5
+    bad[0, 4000] = -1
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B, gpu)
+    ix.build(tabs, torch.from_numpy(bad).reshape(2, B, 1).to(gpu), index_base=0)
+    torch.cuda.synchronize()
+    with pytest.raises(pkg.BoundsError):
+        tabs.ctx.check_bounds()
+    for t, p in ((0, 4000), (1, 17)):
+        got_rows, pos, seg = ix.segments(t)
+        assert p not in pos and seg[-1] == B - 1
+    for k in range(3):
+        idx2 = rand_indices(rng, rows, B, 1)
+        ix.build(tabs, torch.from_numpy(idx2).reshape(2, B, 1).to(gpu), index_base=0)
+        _assert_segments(ix, idx2, B)
 
 
 def test_sgd_update_bitwise_deterministic_and_atomic_close(pkg, gpu):
@@ -384,6 +444,8 @@ def _dt_written_mask(idx, D):
     ([3, 4, 10, 1000, 5_000_000], 128, 2048, 1.1, torch.float32),      # hot rows (multi-slice segments)
     ([5, 100000, 3, 77] * 6 + [9, 10], 128, 300, None, torch.bfloat16),
     ([300, 100000, 5_000_000], 64, 3000, None, torch.float32),         # N > 2048: unsplit fallback
+    ([300, 100000, 3, 5_000_000], 64, 6000, 1.1, torch.float32),       # N > 4096: split hash build
+    ([5, 100000, 3, 77] * 6 + [9, 10], 128, 8192, None, torch.bfloat16),  # configs[2] shape (bf16, B=8192)
     ([50] * 40, 32, 200, None, torch.float32),                         # F = 41: unsplit fallback
     ([1], 16, 64, None, torch.float32)])                               # every position hits one row
 def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
