@@ -115,24 +115,13 @@ def make_inputs(pkg, w, B, dev, rank, T_rows):
     rng = np.random.default_rng(51234 + rank)
     for _ in range(NBATCH):
         if zipf:
-            cols = [torch.from_numpy(zipf_rows(rng, n, B * L, zipf)) for n in T_rows]
+            cols = [torch.from_numpy(pkg.zipf_rows(rng, n, B * L, zipf)) for n in T_rows]
             idx.append(torch.stack(cols).to(dev).contiguous())
             continue
         cols = [torch.randint(0, n, (B * L,), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
                 for n in T_rows]
         idx.append(torch.stack(cols).contiguous())
     return tables, idx, g
-
-
-def zipf_rows(rng, n, size, s):
-    """Zipf(s) ranks (rank 0 hottest, tail folded mod n) scattered over the table's rows by an
-    affine bijection r -> (a*r + c) mod n, so hot rows sit at random places."""
-    z = (rng.zipf(s, size=size) - 1) % n
-    a = int(rng.integers(1, max(n, 2)))
-    while np.gcd(a, n) != 1:
-        a += 1
-    c = int(rng.integers(0, n))
-    return ((z.astype(np.int64) * a + c) % n).astype(np.int32)
 
 
 def cpu_baseline(pkg, w, seconds, threads):
@@ -152,7 +141,7 @@ def cpu_baseline(pkg, w, seconds, threads):
         oracle.fill_uniform(a, -1.0 / np.sqrt(n), 1.0 / np.sqrt(n), 1000 + t, threads)
         tables.append(a)
     if w.get("zipf"):
-        batches = [np.stack([zipf_rows(rng, n, B * L, w["zipf"]) for n in rows]).astype(np.int64) for _ in range(4)]
+        batches = [np.stack([pkg.zipf_rows(rng, n, B * L, w["zipf"]) for n in rows]).astype(np.int64) for _ in range(4)]
     else:
         batches = [np.stack([rng.integers(0, n, size=B * L) for n in rows]).astype(np.int64) for _ in range(4)]
     x = rng.standard_normal((B, D)).astype(np.float32)
@@ -233,9 +222,15 @@ def main():
             engine.step(x, packs[k % NBATCH], dout)
     else:
         from dlrm_jl_amd.sharded import make_bench_engine
-        engine, step = make_bench_engine(pkg, w, B, dev, rank, world, a.lr)
+        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr)
         if a.mode == "graph":
-            a.mode = "eager"  # collectives are launched eagerly (RCCL inside hipGraph capture: not relied on)
+            # the compute between the two all-to-alls is replayed as hipGraphs; the collectives
+            # are launched eagerly (RCCL inside hipGraph capture: not relied on)
+            for k in range(max(a.warmup, 1)):
+                step(k)
+            torch.cuda.synchronize()
+            prepare_graphs()
+            a.mode = "segments"
 
     # warm-up (also validates indices once)
     for k in range(max(a.warmup, 1)):
@@ -422,13 +417,16 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": w["dtype"],
-            "data": "synthetic (uniform indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)",
+            "data": (f"synthetic ({'Zipf(%g) over permuted rows' % w['zipf'] if w.get('zipf') else 'uniform'} "
+                     "indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)"),
             "config": {"workload": a.workload, "tables": T, "dim": D, "batch_per_gpu": B, "global_batch": B * world,
-                       "lookups": L, "index_dtype": "int32", "table_rows": "Criteo-Kaggle (criteo.jl:350-377)",
+                       "lookups": L, "index_dtype": "int32", "table_rows": w.get("rows_src", "Criteo-Kaggle (criteo.jl:350-377)"),
                        "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + RCCL all-to-all",
-                       "launch": f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else "eager",
-                       "ys": ("materialized" if world > 1 or engine.materialize_ys
-                              else "not materialized (backward re-gathers T)"),
+                       "launch": (f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else
+                                  "hipGraph replay of the compute between eager all-to-alls" if a.mode == "segments"
+                                  else "eager"),
+                       "ys": ("received blocks read in place (no ys)" if world > 1 else "materialized"
+                              if engine.materialize_ys else "not materialized (backward re-gathers T)"),
                        "step": ("dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "
                                 "updated in the backward)" if world == 1 and engine.step_api else "operators")},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -357,8 +357,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
-        {(void**)&ix->dev.pslot, hs ? n * 4 : 0},    {(void**)&ix->dev.hkey, (size_t)(T * hs) * 4},
-        {(void**)&ix->dev.hcnt, (size_t)(T * hs) * 4}, {(void**)&ix->dev.hseg, (size_t)(T * hs) * 8},
+        {(void**)&ix->dev.pslot, hs ? n * 4 : 0},    {(void**)&ix->dev.hent, (size_t)(T * hs) * 8},
+        {(void**)&ix->dev.hseg, (size_t)(T * hs) * 8},
         {(void**)&ix->dev.hfill, (size_t)(T * hs) * 4}, {(void**)&ix->dev.hstate, hs ? (size_t)T * 32 : 0},
     };
     size_t total = 0;
@@ -377,7 +377,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         base += (pc.bytes + 255) & ~(size_t)255;
     }
     if (hs) {  // every slot starts empty (the alloc pass resets the slots it used)
-        rc = ctx_hip(ctx, hipMemset(ix->dev.hkey, 0xff, (size_t)(T * hs) * 4), "hipMemset(hash keys)");
+        rc = ctx_hip(ctx, hipMemset(ix->dev.hent, 0xff, (size_t)(T * hs) * 8), "hipMemset(hash slots)");
         if (rc != DLRM_OK) {
             (void)hipFree(ix->block);
             delete ix;

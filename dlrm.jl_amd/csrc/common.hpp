@@ -158,8 +158,7 @@ struct IndexerDev {
     uint8_t* single;       // [T][cap]: 1 = the position's row is hit once in the batch (split builds)
     // hash indexer (hashindex.hip; capacities above the in-LDS build's kFastMaxN)
     int32_t* pslot;        // [T][cap] hash slot of each position (-1: invalid index)
-    uint32_t* hkey;        // [T][hsize] row of each slot, 0xffffffff = empty (reset by the alloc pass)
-    uint32_t* hcnt;        // [T][hsize] positions per slot (reset by the alloc pass)
+    unsigned long long* hent;  // [T][hsize] row << 32 | positions, all ones = empty (reset by the alloc pass)
     int2* hseg;            // [T][hsize] {first perm entry, length} of the slot's segment
     uint32_t* hfill;       // [T][hsize] placement cursor
     unsigned long long* hstate;  // [T][4] {segments << 32 | positions} allocation cursor, ...

@@ -10,8 +10,8 @@
 //
 //   1. insert (tiles of kHixTile positions per workgroup): rows are first merged in an LDS
 //      hash (one entry per distinct row of the tile, with its count), then each distinct row
-//      claims a slot of the table's global open-addressing hash (load <= 1/2, linear probing,
-//      the CAS is the probe) and adds its count there: one CAS + one add per row per tile.
+//      claims a slot of the table's global open-addressing hash (load <= 1/2, linear probing;
+//      64-bit slots row << 32 | count: one CAS for a new row, + one add for a present one).
 //   2. alloc (one thread per slot): occupied slots get a segment {first perm entry, length}
 //      from one 64-bit atomic per workgroup (segment count and position cursor move together,
 //      so seg_start stays monotone); chunk (<= kChunk) / hot (> kChunk) descriptors the same
@@ -27,20 +27,30 @@
 
 namespace dlrm {
 
-constexpr uint32_t kHixEmpty = 0xffffffffu;
+constexpr uint32_t kHixEmpty = 0xffffffffu;  // LDS hash: empty key
 constexpr int kHixRankMax = 256;   // hot segments up to this length: LDS rank sort
 
 __device__ __forceinline__ uint32_t hix_hash(uint32_t r, int hbits) { return (r * 0x9E3779B1u) >> (32 - hbits); }
 
-// Slot of row r (claimed when absent); -1 only if the table were full (load <= 1/2: never).
-// The CAS itself is the probe: it returns the slot's row, so no separate load (a plain load
-// could be served stale from another XCD's L2 anyway).
-__device__ __forceinline__ int hix_probe(uint32_t* hkey, uint32_t r, int hbits) {
+// Adds c positions of row r to its slot (claimed when absent); returns the slot, or -1 only if
+// the table were full (load <= 1/2: never).  A slot is one 64-bit word, row << 32 | count, so
+// a row's first claim is a single CAS that also stores its count; a present row takes one
+// more (no-return) add.  The CAS is the probe (it returns the slot's word): no plain load that
+// another XCD's L2 could serve stale.  Random-address atomics leave L2 one 64-B request each
+// (~20 G/s chip-wide), so their number per row is what this kernel's time is made of.
+constexpr unsigned long long kHixEmpty64 = ~0ull;
+
+__device__ __forceinline__ int hix_insert(unsigned long long* hent, uint32_t r, uint32_t c, int hbits) {
     const uint32_t mask = (hbits >= 32 ? 0xffffffffu : (1u << hbits) - 1u);
     uint32_t h = hix_hash(r, hbits);
+    const unsigned long long mine = ((unsigned long long)r << 32) | c;
     for (uint32_t i = 0; i <= mask; ++i) {
-        const uint32_t old = atomicCAS(hkey + h, kHixEmpty, r);
-        if (old == kHixEmpty || old == r) return (int)h;
+        const unsigned long long old = atomicCAS(hent + h, kHixEmpty64, mine);
+        if (old == kHixEmpty64) return (int)h;
+        if ((uint32_t)(old >> 32) == r) {
+            atomicAdd(hent + h, (unsigned long long)c);
+            return (int)h;
+        }
         h = (h + 1u) & mask;
     }
     return -1;
@@ -109,11 +119,7 @@ __global__ __launch_bounds__(256) void hix_insert_kernel(IndexerDev ix, const Ta
         atomicAdd(&sl.cnt[ls], 1u);
     }
     __syncthreads();
-    if (own) {
-        const int g = hix_probe(ix.hkey + (int64_t)t * ix.hsize, (uint32_t)r, ix.hbits);
-        if (g >= 0) atomicAdd(ix.hcnt + (int64_t)t * ix.hsize + g, sl.cnt[ls]);
-        sl.val[ls] = g;
-    }
+    if (own) sl.val[ls] = hix_insert(ix.hent + (int64_t)t * ix.hsize, (uint32_t)r, sl.cnt[ls], ix.hbits);
     __syncthreads();
     if (p < N) ix.pslot[(int64_t)t * ix.cap + p] = ls >= 0 ? sl.val[ls] : -1;
 }
@@ -131,18 +137,26 @@ __global__ __launch_bounds__(256) void hix_alloc_kernel(IndexerDev ix, int split
     const int t = blockIdx.y;
     const int64_t s0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kHixSPT;
     const int64_t ho = (int64_t)t * ix.hsize;
-    const uint4 cv = *(const uint4*)(ix.hcnt + ho + s0);
-    const uint32_t c[kHixSPT] = {cv.x, cv.y, cv.z, cv.w};
-    uint32_t row[kHixSPT];
+    uint32_t c[kHixSPT], row[kHixSPT];
+    {
+        const ulonglong2 e01 = *(const ulonglong2*)(ix.hent + ho + s0);
+        const ulonglong2 e23 = *(const ulonglong2*)(ix.hent + ho + s0 + 2);
+        const unsigned long long e[kHixSPT] = {e01.x, e01.y, e23.x, e23.y};
+        static_assert(kHixSPT == 4, "two 16-B loads");
+#pragma unroll
+        for (int q = 0; q < kHixSPT; ++q) {
+            c[q] = e[q] == kHixEmpty64 ? 0u : (uint32_t)e[q];
+            row[q] = (uint32_t)(e[q] >> 32);
+        }
+        if (c[0] | c[1] | c[2] | c[3]) {
+            const ulonglong2 ones = make_ulonglong2(kHixEmpty64, kHixEmpty64);
+            *(ulonglong2*)(ix.hent + ho + s0) = ones;
+            *(ulonglong2*)(ix.hent + ho + s0 + 2) = ones;
+        }
+    }
     long long av = 0, bv = 0;
 #pragma unroll
     for (int q = 0; q < kHixSPT; ++q) {
-        row[q] = 0;
-        if (c[q]) {
-            row[q] = ix.hkey[ho + s0 + q];
-            ix.hkey[ho + s0 + q] = kHixEmpty;
-            ix.hcnt[ho + s0 + q] = 0;
-        }
         const bool chunk = c[q] > 0 && c[q] <= (uint32_t)kChunk && !(split && c[q] == 1);
         const bool hot = c[q] > (uint32_t)kChunk;
         const int ns = hot ? (int)((c[q] + kHotSlice - 1) / kHotSlice) : 0;

@@ -2,6 +2,7 @@
 
 Table row counts are the reference's own constants (src/data/criteo.jl:350-406).
 """
+import numpy as np
 
 # src/data/criteo.jl:350-377
 KAGGLE_EMBEDDING_SIZES = [
@@ -33,3 +34,14 @@ WORKLOADS = {
 
 def table_bytes(rows, dim, esize):
     return sum(rows) * dim * esize
+
+
+def zipf_rows(rng, n, size, s):
+    """Zipf(s) ranks (rank 0 hottest, tail folded mod n) scattered over the table's rows by an
+    affine bijection r -> (a*r + c) mod n, so hot rows sit at random places."""
+    z = (rng.zipf(s, size=size) - 1) % n
+    a = int(rng.integers(1, max(n, 2)))
+    while np.gcd(a, n) != 1:
+        a += 1
+    c = int(rng.integers(0, n))
+    return ((z.astype(np.int64) * a + c) % n).astype(np.int32)

@@ -4,21 +4,28 @@ The reference has no distributed code; this is the MI355X extens
 north star asks for: embedding tables shard BY TABLE across ranks, and one all-to-all each
 way moves the looked-up vectors to the ranks that own the samples, and their gradients back.
 
-  rank r owns tables [t0_r, t1_r) (contiguous, balanced count) and samples
-  [r*B, (r+1)*B) of the global batch Bg = world * B (weak scaling: B per GPU is fixed).
+  rank r owns the tables tables(r) (a TablePartition) and samples [r*B, (r+1)*B) of the
+  global batch Bg = world * B (weak scaling: B per GPU is fixed).
 
-  forward : lookup of r's tables for all Bg samples -> send [Bg][T_r*D]
-            all-to-all (row block j -> rank j)      -> recv_j [B][T_j*D] from every rank j
-            scatter into ys [B][F*D] columns D + t0_j*D ...   (x goes in columns 0..D)
-            DotInteraction(x, ys) on the local batch
-  backward: dot_back -> dt [B][F*D]
-            gather dt column blocks per owner -> all-to-all -> grad [Bg][T_r*D]
-            update!(Descent) of r's tables with r's indices for all Bg samples
+  forward : maplookup of r's T_r tables for all Bg samples  -> sbuf [Bg][T_r*D]
+            repack (one copy)                               -> send [world][T_r][B][D]
+            all-to-all (block j -> rank j)                  -> recv = [src j][T_j][B][D]
+            every table's B vectors for r's samples are now one contiguous [B][D] block of
+            recv, i.e. a B-row table whose row b is sample b: the fused lookup+interaction
+            kernel runs on these T "received tables" with identity indices (no ys copy)
+  backward: dot_back re-gathers T from the received tables (dlrm_interact_bwd_gather)
+            -> dt [B][F*D]; repack dt's table columns in owner order (one copy)
+            all-to-all                                      -> grecv [src i][T_r][B][D]
+            repack (one copy)                               -> grad [Bg][T_r*D]
+            update!(Descent) of r's tables with r's indices for all Bg samples; the
+            SparseIndexer (positions grouped by row: a hash build over the whole chip for
+            Bg*L > 4096) is built at the start of the step
 
 All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-ABI kernels)
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
-= RCCL over xGMI on MI355X) carries the two all-to-alls; uneven table counts per rank use
-the split-size form of all_to_all_single.
+= RCCL over xGMI on MI355X) carries the two all-to-alls (uneven table counts per rank: the
+split-size form of all_to_all_single).  The bench replays the compute between the two
+collectives as hipGraphs (`capture`); the collectives themselves are launched eagerly.
 """
 import torch
 import torch.distributed as dist
@@ -26,59 +33,116 @@ import torch.distributed as dist
 from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices
 from .interact import interaction_sizes
-from .runtime import dtype_code, ptr
+from .runtime import context, dtype_code, ptr
+from .shapes import zipf_rows
 from .update import SparseIndexer
 
 
 class TablePartition:
-    """Contiguous, count-balanced assignment of T tables to `world` ranks
-    (every table costs Bg lookups per step whatever its size; Kaggle's largest table is
-    5.2 GB at D=128 fp32, far below one GPU's 288 GB, so count balance is what matters)."""
+    """Assignment of T tables to `world` ranks.
 
-    def __init__(self, T, world):
-        base, extra = divmod(T, world)
-        self.counts = [base + (1 if r < extra else 0) for r in range(world)]
-        self.starts = [sum(self.counts[:r]) for r in range(world)]
+    Default: contiguous, count-balanced blocks (every table costs Bg*L lookups per step
+    whatever its size, so equal counts balance the gather, the exchange and the update).
+    `TablePartition.fitting(rows, world, row_bytes, capacity)` keeps that when every block
+    fits in `capacity` bytes and otherwise assigns tables largest-first to the rank with the
+    fewest bytes (ties: fewest tables) -- e.g. Criteo-Terabyte fp32 on 2 GPUs, whose
+    contiguous halves are 185 and 267 GB (criteo.jl:379-406)."""
+
+    def __init__(self, T, world, owners=None):
         self.T, self.world = T, world
+        if owners is None:
+            base, extra = divmod(T, world)
+            counts = [base + (1 if r < extra else 0) for r in range(world)]
+            starts = [sum(counts[:r]) for r in range(world)]
+            owners = [list(range(starts[r], starts[r] + counts[r])) for r in range(world)]
+        if sorted(t for o in owners for t in o) != list(range(T)) or len(owners) != world:
+            raise ValueError("every table must be owned by exactly one rank")
+        self.owners = [list(o) for o in owners]
+        self.counts = [len(o) for o in self.owners]
+        self.order = [t for o in self.owners for t in o]  # tables in exchange-block order
+        self.contiguous = self.order == list(range(T)) and all(
+            o == list(range(o[0], o[0] + len(o))) for o in self.owners if o)
+
+    @classmethod
+    def fitting(cls, rows, world, row_bytes, capacity):
+        p = cls(len(rows), world)
+        if max(sum(rows[t] for t in o) * row_bytes for o in p.owners) <= capacity:
+            return p
+        load = [0] * world
+        owners = [[] for _ in range(world)]
+        for t in sorted(range(len(rows)), key=lambda t: -rows[t]):
+            r = min(range(world), key=lambda r: (load[r], len(owners[r])))
+            owners[r].append(t)
+            load[r] += rows[t]
+        return cls(len(rows), world, [sorted(o) for o in owners])
+
+    def tables(self, r):
+        return self.owners[r]
 
     def range(self, r):
-        return self.starts[r], self.starts[r] + self.counts[r]
+        """[t0, t1) of rank r (contiguous partitions only)."""
+        if not self.contiguous:
+            raise ValueError("range(): this partition is not contiguous; use tables(r)")
+        o = self.owners[r]
+        return (o[0], o[0] + len(o)) if o else (sum(self.counts[:r]), sum(self.counts[:r]))
+
+    def bytes_per_rank(self, rows, row_bytes):
+        return [sum(rows[t] for t in o) * row_bytes for o in self.owners]
 
 
 class HipShardOps:
     """The product ops: the HIP kernels behind include/dlrm_hip.h (no host syncs)."""
 
-    def __init__(self, tables, batch_global, lookups, lr, index_base=0):
-        self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
-        self.ctx = self.ts.ctx
+    def __init__(self, tables, batch_global, lookups, lr, index_base=0, device=None):
+        tables = list(tables)
+        self.ts = EmbeddingTableSet(tables) if tables else None
+        self.device = self.ts.device if self.ts else torch.device(device)
+        self.ctx = self.ts.ctx if self.ts else context(self.device)
         self.lib = self.ctx.lib
         self.Bg, self.L, self.lr, self.base = batch_global, lookups, lr, index_base
-        self.indexer = SparseIndexer(len(self.ts), batch_global * lookups, self.ts.device)
+        self.indexer = SparseIndexer(len(tables), batch_global * lookups, self.device) if tables else None
+        self.rts = self.ident = None
 
     def _ok(self, rc):
         if rc != _lib.OK:
             self.ctx.check(rc)
 
+    def bind_recv(self, tabs):
+        """tabs: the T received [B][D] blocks in global table order (views of one buffer)."""
+        self.rts = EmbeddingTableSet(tabs)
+        T, B = len(tabs), tabs[0].shape[0]
+        ar = torch.arange(B, dtype=torch.int32, device=self.device)
+        self.ident = PackedIndices(ar.repeat(T, 1).reshape(T, B, 1))
+
+    def build_indexer(self, idx):
+        self._ok(self.lib.dlrm_indexer_build(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
+                                             idx.itype, idx.stride, self.base, idx.B, idx.L))
+
     def lookup(self, idx, send):
         self._ok(self.lib.dlrm_maplookup(self.ctx.bind(), self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
                                          self.base, idx.B, idx.L, ptr(send), send.stride(0), 0))
 
-    def interact_fwd(self, x, ys, out, padding):
-        d = x.shape[1]
-        self._ok(self.lib.dlrm_interact_fwd(self.ctx.bind(), dtype_code(x.dtype), d, ys.shape[1] // d, x.shape[0],
-                                            ptr(x), x.stride(0), ptr(ys), ys.stride(0), ptr(out), out.stride(0),
-                                            padding))
+    def interact_fwd_recv(self, x, out, padding):
+        i = self.ident
+        self._ok(self.lib.dlrm_lookup_interact_fwd(self.ctx.bind(), self.rts.handle, ptr(i.data), i.itype, i.stride,
+                                                   0, i.B, 1, ptr(x), x.stride(0), None, 0, ptr(out), out.stride(0),
+                                                   padding))
 
-    def interact_bwd(self, dout, ys, dx, dt, padding):
-        d = dx.shape[1]
-        self._ok(self.lib.dlrm_interact_bwd(self.ctx.bind(), dtype_code(dout.dtype), d, ys.shape[1] // d,
-                                            dout.shape[0], ptr(dout), dout.stride(0), padding, ptr(ys), ys.stride(0),
-                                            ptr(dx), dx.stride(0), ptr(dt), dt.stride(0)))
+    def interact_bwd_recv(self, dout, x, dx, dt, padding):
+        i = self.ident
+        self._ok(self.lib.dlrm_interact_bwd_gather(self.ctx.bind(), self.rts.handle, None, ptr(i.data), i.itype,
+                                                   i.stride, 0, i.B, 1, ptr(x), x.stride(0), ptr(dout),
+                                                   dout.stride(0), padding, ptr(dx), dx.stride(0), ptr(dt),
+                                                   dt.stride(0)))
 
-    def update(self, idx, grad):
-        self._ok(self.lib.dlrm_sgd_update(self.ctx.bind(), self.ts.handle, self.indexer.handle, 0, ptr(idx.data),
+    def update(self, idx, grad, prebuilt=False):
+        flags = _lib.UPDATE_PREBUILT if prebuilt else 0
+        self._ok(self.lib.dlrm_sgd_update(self.ctx.bind(), self.ts.handle, self.indexer.handle, flags, ptr(idx.data),
                                           idx.itype, idx.stride, self.base, idx.B, idx.L, ptr(grad),
                                           dtype_code(grad.dtype), grad.stride(0), 0, self.lr))
+
+    def check_bounds(self):
+        self.ctx.check_bounds()
 
 
 class ShardedHotPath:
@@ -91,26 +155,32 @@ class ShardedHotPath:
         self.Bg = batch_local * self.world
         self.T = partition.T
         self.F = self.T + 1
-        self.t0, self.t1 = partition.range(rank)
-        self.Tr = self.t1 - self.t0
+        self.mine = partition.tables(rank)
+        self.Tr = len(self.mine)
         self.group = group
         _, self.width, self.padding = interaction_sizes(dim, self.F)
         dev = device
-        D, B = dim, batch_local
-        self.send = torch.empty((self.Bg, max(self.Tr, 1) * D), dtype=dtype, device=dev)
-        self.recv = torch.empty((sum(c * B * D for c in partition.counts),), dtype=dtype, device=dev)
-        self.ys = torch.zeros((B, self.F * D), dtype=dtype, device=dev)
+        D, B, T, Tr, W = dim, batch_local, self.T, self.Tr, self.world
+        self.sbuf = torch.empty((self.Bg, max(Tr, 1) * D), dtype=dtype, device=dev)
+        self.send = torch.empty((W * Tr * B * D,), dtype=dtype, device=dev)
+        self.recv = torch.empty((T * B * D,), dtype=dtype, device=dev)
         self.out = torch.empty((B, self.width), dtype=dtype, device=dev)
         self.dx = torch.empty((B, D), dtype=torch.float32, device=dev)
         self.dt = torch.empty((B, self.F * D), dtype=torch.float32, device=dev)
-        self.gsend = torch.empty((sum(c * B * D for c in partition.counts),), dtype=torch.float32, device=dev)
-        self.grecv = torch.empty((self.Bg, max(self.Tr, 1) * D), dtype=torch.float32, device=dev)
+        self.gsend = torch.empty((T * B * D,), dtype=torch.float32, device=dev)
+        self.grecv = torch.empty((W * Tr * B * D,), dtype=torch.float32, device=dev)
+        self.grad = torch.empty((self.Bg, max(Tr, 1) * D), dtype=torch.float32, device=dev)
         # element counts of each peer's block (flat all_to_all_single splits)
-        self.fwd_in_splits = [B * self.Tr * D] * self.world
-        self.fwd_out_splits = [B * c * D for c in partition.counts]
+        self.fwd_in_splits = [Tr * B * D] * W
+        self.fwd_out_splits = [c * B * D for c in partition.counts]
         self.bwd_in_splits = self.fwd_out_splits
         self.bwd_out_splits = self.fwd_in_splits
-        self.offsets = [sum(self.fwd_out_splits[:j]) for j in range(self.world)]
+        # received block of global table t: position of t in the exchange order
+        slot = {t: i for i, t in enumerate(partition.order)}
+        self.recv_tables = [self.recv[slot[t] * B * D:(slot[t] + 1) * B * D].view(B, D) for t in range(T)]
+        self.order = None if partition.order == list(range(T)) else torch.tensor(partition.order, device=dev)
+        ops.bind_recv(self.recv_tables)
+        self._graphs = None
 
     # ---- exchange (pure data movement; identical for every ShardOps)
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -123,80 +193,145 @@ class ShardedHotPath:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
+    def pack_send(self):
+        """sbuf [Bg][T_r*D] (sample-major) -> send [world][T_r][B][D]."""
+        if self.Tr:
+            W, B, Tr, D = self.world, self.B, self.Tr, self.D
+            self.send.view(W, Tr, B, D).copy_(self.sbuf.view(W, B, Tr, D).permute(0, 2, 1, 3))
+
     def exchange_fwd(self):
-        self._a2a(self.recv, self.send.reshape(-1)[: self.Bg * self.Tr * self.D], self.fwd_out_splits,
-                  self.fwd_in_splits)
-        D, B = self.D, self.B
-        for j in range(self.world):
-            c = self.part.counts[j]
-            if c == 0:
-                continue
-            t0, _ = self.part.range(j)
-            blk = self.recv[self.offsets[j]: self.offsets[j] + B * c * D].view(B, c * D)
-            self.ys[:, D + t0 * D: D + (t0 + c) * D].copy_(blk)
+        self._a2a(self.recv, self.send, self.fwd_out_splits, self.fwd_in_splits)
+
+    def pack_grad(self):
+        """dt's table columns [B][T][D] -> gsend [T][B][D] in exchange order."""
+        B, T, D = self.B, self.T, self.D
+        dt3 = self.dt[:, D:].view(B, T, D).permute(1, 0, 2)
+        if self.order is not None:
+            dt3 = dt3[self.order]
+        self.gsend.view(T, B, D).copy_(dt3)
 
     def exchange_bwd(self):
-        D, B = self.D, self.B
-        for j in range(self.world):
-            c = self.part.counts[j]
-            if c == 0:
-                continue
-            t0, _ = self.part.range(j)
-            self.gsend[self.offsets[j]: self.offsets[j] + B * c * D].view(B, c * D).copy_(
-                self.dt[:, D + t0 * D: D + (t0 + c) * D])
-        self._a2a(self.grecv.reshape(-1)[: self.Bg * self.Tr * self.D], self.gsend, self.bwd_out_splits,
-                  self.bwd_in_splits)
+        self._a2a(self.grecv, self.gsend, self.bwd_out_splits, self.bwd_in_splits)
 
-    # ---- the step
-    def forward(self, x, idx):
+    def unpack_grad(self):
+        """grecv [world][T_r][B][D] -> grad [Bg][T_r*D] (sample-major, as the update reads it)."""
+        if self.Tr:
+            W, B, Tr, D = self.world, self.B, self.Tr, self.D
+            self.grad.view(W, B, Tr, D).copy_(self.grecv.view(W, Tr, B, D).permute(0, 2, 1, 3))
+
+    # ---- the step, as three compute segments around the two exchanges
+    def seg_lookup(self, idx):
         """idx: PackedIndices of this rank's tables for the GLOBAL batch ([T_r][Bg*L])."""
         if self.Tr:
-            self.ops.lookup(idx, self.send)
+            self.ops.build_indexer(idx)  # depends on the indices only
+            self.ops.lookup(idx, self.sbuf)
+            self.pack_send()
+
+    def seg_interact(self, x, dout):
+        self.ops.interact_fwd_recv(x, self.out, self.padding)
+        self.ops.interact_bwd_recv(dout, x, self.dx, self.dt, self.padding)
+        self.pack_grad()
+
+    def seg_update(self, idx):
+        if self.Tr:
+            self.unpack_grad()
+            self.ops.update(idx, self.grad, prebuilt=True)
+
+    def forward(self, x, idx):
+        self.seg_lookup(idx)
         self.exchange_fwd()
-        self.ops.interact_fwd(x, self.ys, self.out, self.padding)
+        self.ops.interact_fwd_recv(x, self.out, self.padding)
         return self.out
 
-    def backward(self, idx, dout):
-        self.ops.interact_bwd(dout, self.ys, self.dx, self.dt, self.padding)
+    def backward(self, idx, dout, x):
+        self.ops.interact_bwd_recv(dout, x, self.dx, self.dt, self.padding)
+        self.pack_grad()
         self.exchange_bwd()
-        if self.Tr:
-            self.ops.update(idx, self.grecv)
+        self.seg_update(idx)
         return self.dx
 
     def step(self, x, idx, dout):
-        self.forward(x, idx)
-        return self.backward(idx, dout)
+        self.seg_lookup(idx)
+        self.exchange_fwd()
+        self.seg_interact(x, dout)
+        self.exchange_bwd()
+        self.seg_update(idx)
+        return self.dx
+
+    # ---- hipGraph replay of the compute segments (collectives stay eager)
+    def capture(self, x, idx_list, dout):
+        """Captures seg_lookup / seg_update per index batch and seg_interact once."""
+        s = torch.cuda.Stream(device=self.sbuf.device)
+        s.wait_stream(torch.cuda.current_stream())
+        look, upd = [], []
+        with torch.cuda.stream(s):
+            for idx in idx_list:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self.seg_lookup(idx)
+                look.append(g)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self.seg_update(idx)
+                upd.append(g)
+            mid = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(mid, stream=s):
+                self.seg_interact(x, dout)
+        torch.cuda.current_stream().wait_stream(s)
+        self._graphs = (look, mid, upd)
+
+    def step_graphed(self, k):
+        look, mid, upd = self._graphs
+        look[k].replay()
+        self.exchange_fwd()
+        mid.replay()
+        self.exchange_bwd()
+        upd[k].replay()
 
 
-def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234):
+def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None):
     """Bench setup for one rank: local tables (full size) and NBATCH index batches for the
-    global batch; returns (engine, step(k) closure)."""
+    global batch; returns (engine, step(k) closure, prepare_graphs() closure)."""
     import numpy as np
     rows = w["rows"]
     D, L = w["dim"], w["lookups"]
-    part = TablePartition(len(rows), world)
-    t0, t1 = part.range(rank)
+    E = 4 if w["dtype"] == "f32" else 2
+    if capacity is None:
+        capacity = int(torch.cuda.get_device_properties(device).total_memory * 0.85)
+    part = TablePartition.fitting(rows, world, D * E, capacity)
+    mine = part.tables(rank)
     dt = torch.float32 if w["dtype"] == "f32" else torch.bfloat16
     g = torch.Generator(device=device).manual_seed(seed + rank)
     tables = []
-    for n in rows[t0:t1]:
+    for t in mine:
+        n = rows[t]
         s = 1.0 / float(np.sqrt(n))
-        t = torch.empty((n, D), dtype=torch.float32, device=device).uniform_(-s, s, generator=g)
-        tables.append(t.to(dt))
+        tables.append(torch.empty((n, D), dtype=dt, device=device).uniform_(-s, s, generator=g))
     Bg = batch_local * world
-    ops = HipShardOps(tables, Bg, L, lr) if tables else None
+    ops = HipShardOps(tables, Bg, L, lr, device=device)
     eng = ShardedHotPath(ops, part, rank, batch_local, D, L, dt, device)
     nb = 8
     packs = []
+    zipf = w.get("zipf")
+    rng = np.random.default_rng(seed + rank)
     for _ in range(nb):
-        cols = [torch.randint(0, n, (Bg * L,), device=device, generator=g, dtype=torch.int64).to(torch.int32)
-                for n in rows[t0:t1]]
+        if zipf:
+            cols = [torch.from_numpy(zipf_rows(rng, rows[t], Bg * L, zipf)).to(device) for t in mine]
+        else:
+            cols = [torch.randint(0, rows[t], (Bg * L,), device=device, generator=g,
+                                  dtype=torch.int64).to(torch.int32) for t in mine]
         data = torch.stack(cols) if cols else torch.zeros((0, Bg * L), dtype=torch.int32, device=device)
         packs.append(PackedIndices(data.reshape(len(cols), Bg, L)))
     x = torch.randn((batch_local, D), device=device, generator=g).to(dt)
     dout = (torch.randn((batch_local, eng.width), device=device, generator=g) * 1e-3).to(dt)
 
     def step(k):
-        eng.step(x, packs[k % nb], dout)
+        if eng._graphs is not None:
+            eng.step_graphed(k % nb)
+        else:
+            eng.step(x, packs[k % nb], dout)
 
-    return eng, step
+    def prepare_graphs():
+        eng.capture(x, packs, dout)
+
+    return eng, step, prepare_graphs

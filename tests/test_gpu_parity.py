@@ -631,7 +631,7 @@ def test_host_tensors_are_rejected_before_launch(pkg, gpu):
 
 
 # ------------------------------------------------------------------ sharded (2 ranks on one GPU)
-def _gpu_shard_worker(rank, world, port, outdir):
+def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False):
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -651,23 +651,30 @@ def _gpu_shard_worker(rank, world, port, outdir):
     x = rng.standard_normal((Bg, D)).astype(np.float32)
     F = T + 1
     dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
-    part = TablePartition(T, world)
-    t0, t1 = part.range(rank)
-    ops = HipShardOps([torch.from_numpy(t).to(dev) for t in tabs[t0:t1]], Bg, L, 0.25)
+    part = TablePartition(T, world, owners)
+    mine = part.tables(rank)
+    ops = HipShardOps([torch.from_numpy(tabs[t]).to(dev) for t in mine], Bg, L, 0.25, device=dev)
     eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, dev)
-    p = pkg.PackedIndices(torch.from_numpy(idx[t0:t1]).to(torch.int32).reshape(t1 - t0, Bg, L).to(dev))
+    p = pkg.PackedIndices(torch.from_numpy(idx[mine]).to(torch.int32).reshape(len(mine), Bg, L).to(dev))
     sl = slice(rank * B, (rank + 1) * B)
-    eng.step(torch.from_numpy(x[sl]).to(dev), p, torch.from_numpy(dout[sl]).to(dev))
+    xd, dd = torch.from_numpy(x[sl]).to(dev), torch.from_numpy(dout[sl]).to(dev)
+    if graphed:  # the bench's form: compute segments replayed as hipGraphs around eager exchanges
+        eng.capture(xd, [p], dd)
+        eng.step_graphed(0)
+    else:
+        eng.step(xd, p, dd)
     torch.cuda.synchronize()
     ops.ctx.check_bounds()
     np.savez(os.path.join(outdir, f"g{rank}.npz"), out=eng.out.cpu().numpy(), dx=eng.dx.cpu().numpy(),
-             **{f"t{t}": ops.ts[t - t0].data.cpu().numpy() for t in range(t0, t1)})
+             **{f"t{t}": ops.ts[k].data.cpu().numpy() for k, t in enumerate(mine)})
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path):
-    """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange) equals the
+@pytest.mark.parametrize("owners,graphed", [(None, False), ([[4, 0, 2], [1, 3]], True)])
+def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed):
+    """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange; contiguous
+    or byte-balanced table assignment; eager or hipGraph-segment launches) equals the
     single-GPU HotPath on the global batch bit for bit."""
     import socket
     import torch.multiprocessing as mp
@@ -676,7 +683,8 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path):
     port = s.getsockname()[1]
     s.close()
     world = 2
-    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method="spawn")
+    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path), owners, graphed), nprocs=world,
+                       start_method="spawn")
     rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 64, 2
     T, Bg = len(rows), B * world
     rng = np.random.default_rng(7)
@@ -689,11 +697,11 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path):
     p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(T, Bg, L).to(gpu))
     hp.step(torch.from_numpy(x).to(gpu), p, torch.from_numpy(dout).to(gpu))
     from dlrm_jl_amd.sharded import TablePartition
-    part = TablePartition(T, world)
+    part = TablePartition(T, world, owners)
     for r in range(world):
         z = np.load(tmp_path / f"g{r}.npz")
         sl = slice(r * B, (r + 1) * B)
         assert np.array_equal(z["out"], to_np_f32(hp.out)[sl])
         assert np.array_equal(z["dx"], to_np_f32(hp.dx)[sl])
-        for t in range(*part.range(r)):
+        for t in part.tables(r):
             assert np.array_equal(z[f"t{t}"], to_np_f32(hp.ts[t].data)), (r, t)

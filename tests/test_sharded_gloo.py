@@ -34,21 +34,30 @@ class OracleShardOps:
         self.tables = tables
         self.lr = lr
 
+    def bind_recv(self, tabs):
+        self.recv_tables = tabs
+
+    def build_indexer(self, idx):
+        pass
+
     def lookup(self, idx, send):
         self.o.maplookup(self.tables, idx.data.numpy().astype(np.int64), 0, idx.B, idx.L, send.numpy(), 0)
 
-    def interact_fwd(self, x, ys, out, padding):
-        d = x.shape[1]
-        res = self.o.interact_fwd(x.numpy(), ys.numpy(), ys.shape[1] // d, padding)
+    def _ys(self, x):
+        return torch.cat([x] + list(self.recv_tables), dim=1).numpy()
+
+    def interact_fwd_recv(self, x, out, padding):
+        ys = self._ys(x)
+        res = self.o.interact_fwd(x.numpy(), ys, len(self.recv_tables) + 1, padding)
         out.copy_(torch.from_numpy(res))
 
-    def interact_bwd(self, dout, ys, dx, dt, padding):
+    def interact_bwd_recv(self, dout, x, dx, dt, padding):
         d = dx.shape[1]
-        rdx, rdt = self.o.interact_bwd(dout.numpy(), ys.numpy(), d, ys.shape[1] // d, padding)
+        rdx, rdt = self.o.interact_bwd(dout.numpy(), self._ys(x), d, len(self.recv_tables) + 1, padding)
         dx.copy_(torch.from_numpy(rdx))
         dt.copy_(torch.from_numpy(rdt))
 
-    def update(self, idx, grad):
+    def update(self, idx, grad, prebuilt=False):
         self.o.sgd_update(self.tables, idx.data.numpy().astype(np.int64), 0, idx.B, idx.L, grad.numpy(), 0, self.lr)
 
 
@@ -70,27 +79,29 @@ def _worker(rank, world, port, cfg, outdir):
     import dlrm_pkg
     pkg = dlrm_pkg.load()
     from dlrm_jl_amd.sharded import ShardedHotPath, TablePartition
-    T, rows, D, B, L, lr = cfg
+    T, rows, D, B, L, lr, owners = cfg
     tables, idx, x, dout = _problem(T, rows, D, B, world, L)
-    part = TablePartition(T, world)
-    t0, t1 = part.range(rank)
-    ops = OracleShardOps([tables[t].copy() for t in range(t0, t1)], lr)
+    part = TablePartition(T, world, owners)
+    mine = part.tables(rank)
+    ops = OracleShardOps([tables[t].copy() for t in mine], lr)
     eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, torch.device("cpu"))
-    p = pkg.PackedIndices(torch.from_numpy(idx[t0:t1]).reshape(t1 - t0, B * world, L))
+    p = pkg.PackedIndices(torch.from_numpy(idx[mine]).reshape(len(mine), B * world, L))
     sl = slice(rank * B, (rank + 1) * B)
     eng.step(torch.from_numpy(x[sl]).contiguous(), p, torch.from_numpy(dout[sl]).contiguous())
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), out=eng.out.numpy(), dx=eng.dx.numpy(),
-             **{f"table{t}": ops.tables[t - t0] for t in range(t0, t1)})
+             **{f"table{t}": ops.tables[k] for k, t in enumerate(mine)})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,T,L", [(2, 5, 1), (2, 7, 3), (3, 4, 1), (3, 2, 2)])
-def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L):
+@pytest.mark.parametrize("world,T,L,owners", [(2, 5, 1, None), (2, 7, 3, None), (3, 4, 1, None), (3, 2, 2, None),
+                                               (2, 5, 1, [[4, 0, 2], [1, 3]]), (3, 6, 2, [[5], [0, 2, 3, 4], [1]])])
+def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners):
+    """owners: explicit (non-contiguous) table assignment, as TablePartition.fitting makes."""
     import oracle
     rows = [3, 50, 1000, 7, 400, 12, 90][:T]
     D, B, lr = 16, 4, 0.5
-    cfg = (T, rows, D, B, L, lr)
+    cfg = (T, rows, D, B, L, lr, owners)
     mp.start_processes(_worker, args=(world, _free_port(), cfg, str(tmp_path)), nprocs=world, start_method="spawn")
     # single process on the global batch
     tables, idx, x, dout = _problem(T, rows, D, B, world, L)
@@ -102,14 +113,13 @@ def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L):
     dx, dt = oracle.interact_bwd(dout, ys, D, F)
     oracle.sgd_update(tables, idx, 0, Bg, L, dt, D, lr)
     from dlrm_jl_amd.sharded import TablePartition
-    part = TablePartition(T, world)
+    part = TablePartition(T, world, owners)
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")
         sl = slice(r * B, (r + 1) * B)
         assert np.array_equal(z["out"], out[sl])
         assert np.array_equal(z["dx"], dx[sl])
-        t0, t1 = part.range(r)
-        for t in range(t0, t1):
+        for t in part.tables(r):
             assert np.array_equal(z[f"table{t}"], tables[t]), (r, t)
 
 
@@ -122,3 +132,22 @@ def test_table_partition_is_balanced_and_contiguous():
         assert sum(p.counts) == T and max(p.counts) - min(p.counts) <= 1
         covered = [t for r in range(W) for t in range(*p.range(r))]
         assert covered == list(range(T))
+
+
+def test_partition_fits_terabyte_tables():
+    """Criteo-Terabyte (criteo.jl:379-406) at D=128 fp32: the contiguous blocks fit 288 GB at 4
+    and 8 GPUs; at 2 GPUs (267 GB block) the byte-balanced assignment is used instead."""
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import TablePartition
+    rows = pkg.TERABYTE_EMBEDDING_SIZES
+    rb, cap = 128 * 4, int(288e9 * 0.85)
+    for W in (2, 4, 8):
+        p = TablePartition.fitting(rows, W, rb, cap)
+        per = p.bytes_per_rank(rows, rb)
+        assert max(per) <= cap and sorted(p.order) == list(range(26))
+        assert p.contiguous == (W != 2)
+    p2 = TablePartition.fitting(rows, 2, rb, cap)
+    assert max(p2.bytes_per_rank(rows, rb)) < 240e9
+    with pytest.raises(ValueError):
+        TablePartition(3, 2, [[0, 1], [1, 2]])
