@@ -58,6 +58,9 @@ SIGNATURES = {
     "dlrm_tables_create": (_i32, [_vp, _i32, _i32, _i32, _pp, _pi64, _pp]),
     "dlrm_tables_destroy": (_i32, [_vp]),
     "dlrm_maplookup": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _i64]),
+    "dlrm_maplookup_blocked": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _i64,
+                                      _i64]),
+    "dlrm_scatter_rows": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp]),
     "dlrm_interact_fwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_lookup_interact_fwd": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64,
                                          _i32]),

@@ -246,6 +246,37 @@ int dlrm_maplookup(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, in
                             index_base, batch, lookups, out, out_ld, out_offset);
 }
 
+int dlrm_maplookup_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
+                           int64_t table_stride, int index_base, int batch, int lookups, void* out, int64_t out_ld,
+                           int64_t out_offset, int64_t out_table_stride, int64_t block_rows, int64_t block_stride) {
+    CHECK_ARG(ctx && tb, "dlrm_maplookup_blocked: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, lookups);
+    if (rc) return rc;
+    CHECK_ARG(batch == 0 || tb->T == 0 || out, "dlrm_maplookup_blocked: null out");
+    CHECK_ARG(out_ld >= 0 && out_offset >= 0 && out_table_stride >= 0 && block_rows > 0 && block_stride >= 0,
+              "dlrm_maplookup_blocked: negative stride or block_rows < 1");
+    return launch_maplookup_map(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype,
+                                table_stride, index_base, batch, lookups, out,
+                                OutMap{out_ld, out_offset, out_table_stride, block_rows, block_stride});
+}
+
+int dlrm_scatter_rows(dlrm_ctx* ctx, int esize, int num_tables, int batch, int dim, const void* src, int64_t src_ld,
+                      int64_t src_offset, void* dst, const int64_t* dst_base, const int64_t* dst_ld) {
+    CHECK_ARG(ctx, "dlrm_scatter_rows: null ctx");
+    CHECK_ARG(esize == 2 || esize == 4, "dlrm_scatter_rows: esize %d", esize);
+    CHECK_ARG(num_tables >= 0 && batch >= 0 && dim >= 0 && src_ld >= 0 && src_offset >= 0,
+              "dlrm_scatter_rows: negative size");
+    CHECK_ARG(num_tables == 0 || batch == 0 || dim == 0 || (src && dst && dst_base && dst_ld),
+              "dlrm_scatter_rows: null buffer");
+    // 16-B pieces when the source rows allow (a destination row that is not 16-B aligned is
+    // copied element by element on the device)
+    const int u = 16 / esize;
+    const bool vec = (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 && src_ld % u == 0 && src_offset % u == 0 &&
+                     dim % u == 0;
+    return launch_scatter_rows(ctx, esize, num_tables, batch, dim, src, src_ld, src_offset, dst, dst_base, dst_ld,
+                               vec);
+}
+
 // ---------------------------------------------------------------------- interaction
 int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* x, int64_t x_ld,
                       void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {

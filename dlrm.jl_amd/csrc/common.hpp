@@ -140,6 +140,18 @@ __device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
 
 namespace dlrm {
 // Per-table indexer arrays (device), each [T][cap] (seg_start [T][cap+1]).
+// Output row addressing of a lookup: row b of table t lands at
+//   (b / brows) * bstride + (b % brows) * ld + off + t * tstride
+// (plain [B][ld] rows: tstride = D, brows >= B; the sharded send layout [peer][table][b][D]:
+// ld = D, tstride = B_local * D, brows = B_local, bstride = T_r * B_local * D).
+struct OutMap {
+    int64_t ld, off, tstride, brows, bstride;
+    __device__ __forceinline__ int64_t row(int64_t b) const {
+        const int64_t q = b / brows;
+        return q * bstride + (b - q * brows) * ld + off;
+    }
+};
+
 constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions per table
 constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
 
@@ -207,6 +219,11 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int64_t hix_table_slots(int64_t cap);
 int launch_hix_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
                      int64_t tstride, int base, int N, bool split);
+int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
+                         const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
+                         const OutMap& om);
+int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const void* src, int64_t src_ld,
+                        int64_t src_off, void* dst, const int64_t* dbase, const int64_t* dld, bool vec_ok);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
                          int itype, int64_t tstride, int base, int B, int L);
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,

@@ -21,8 +21,7 @@ template <typename T, int VPR, int U>
 __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict__ tabs, int ntab,
                                                      const void* __restrict__ idx, int itype,
                                                      int64_t tstride, int base, int B, int L,
-                                                     T* __restrict__ out, int64_t out_ld, int64_t out_off,
-                                                     unsigned* __restrict__ err) {
+                                                     T* __restrict__ out, OutMap om, unsigned* __restrict__ err) {
     typedef Vec<T> V;
     constexpr int NE = V::N;                       // elements per 16-B vector
     constexpr int LPR = VPR <= 64 ? VPR : 64;      // lanes per row
@@ -81,7 +80,7 @@ __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict
             if (!live[u]) continue;
             const int64_t b = item[u] / ntab;
             const int t = (int)(item[u] - b * ntab);
-            T* o = out + b * out_ld + out_off + (int64_t)t * D;
+            T* o = out + om.row(b) + (int64_t)t * om.tstride;
 #pragma unroll
             for (int j = 0; j < VPL; ++j) *((typename V::type*)o + v + j * 64) = V::from_f32(acc[u][j]);
         }
@@ -93,8 +92,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void maplookup_scalar(const TableDesc* __restrict__ tabs, int ntab, int D,
                                                         const void* __restrict__ idx, int itype,
                                                         int64_t tstride, int base, int B, int L,
-                                                        T* __restrict__ out, int64_t out_ld, int64_t out_off,
-                                                        unsigned* __restrict__ err) {
+                                                        T* __restrict__ out, OutMap om, unsigned* __restrict__ err) {
     const int64_t total = (int64_t)ntab * B * D;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
@@ -110,14 +108,13 @@ __global__ __launch_bounds__(256) void maplookup_scalar(const TableDesc* __restr
             else if (c == 0) raise_index_error(err);
             acc = (k == 0) ? f : acc + f;
         }
-        out[b * out_ld + out_off + (int64_t)t * D + c] = from_f32<T>(acc);
+        out[om.row(b) + (int64_t)t * om.tstride + c] = from_f32<T>(acc);
     }
 }
 
 template <typename T, int VPR>
 static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx, int itype,
-                       int64_t tstride, int base, int B, int L, void* out, int64_t out_ld, int64_t out_off,
-                       unsigned* err) {
+                       int64_t tstride, int base, int B, int L, void* out, const OutMap& om, unsigned* err) {
     constexpr int LPR = VPR <= 64 ? VPR : 64;
     constexpr int RPW = 64 / LPR;
     constexpr int U = 4;
@@ -128,15 +125,15 @@ static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, int T_, co
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL((maplookup_vec<T, VPR, U>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx, itype,
-                       tstride, base, B, L, (T*)out, out_ld, out_off, err);
+                       tstride, base, B, L, (T*)out, om, err);
 }
 
 template <typename T>
 static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx,
-                         int itype, int64_t tstride, int base, int B, int L, void* out, int64_t out_ld,
-                         int64_t out_off, unsigned* err) {
+                         int itype, int64_t tstride, int base, int B, int L, void* out, const OutMap& om,
+                         unsigned* err) {
 #define DLRM_CASE(N) \
-    case N: launch_vec<T, N>(s, cus, tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err); return true;
+    case N: launch_vec<T, N>(s, cus, tabs, T_, idx, itype, tstride, base, B, L, out, om, err); return true;
     switch (vpr) {
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64)
         DLRM_CASE(128) DLRM_CASE(256)
@@ -148,19 +145,27 @@ static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs,
 int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T_, int D, int dtype,
                      const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
                      int64_t out_ld, int64_t out_off) {
+    return launch_maplookup_map(ctx, d_tabs, tabs_aligned16, T_, D, dtype, idx, itype, tstride, base, B, L, out,
+                                OutMap{out_ld, out_off, D, B > 0 ? B : 1, 0});
+}
+
+int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T_, int D, int dtype,
+                         const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
+                         const OutMap& om) {
     if (T_ == 0 || B == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     unsigned* err = ctx_error_word(ctx);
     const int cus = ctx_num_cus(ctx);
     const int esz = dtype == DLRM_F32 ? 4 : 2;
-    const bool aligned = tabs_aligned16 && ((uintptr_t)out % 16 == 0) && ((out_ld * esz) % 16 == 0) &&
-                         ((out_off * esz) % 16 == 0) && ((D * esz) % 16 == 0);
+    const bool aligned = tabs_aligned16 && ((uintptr_t)out % 16 == 0) && ((om.ld * esz) % 16 == 0) &&
+                         ((om.off * esz) % 16 == 0) && ((om.tstride * esz) % 16 == 0) &&
+                         ((om.bstride * esz) % 16 == 0) && ((D * esz) % 16 == 0);
     bool done = false;
     if (aligned) {
         const int vpr = D * esz / 16;
         done = dtype == DLRM_F32
-                   ? dispatch_vec<float>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err)
-                   : dispatch_vec<uint16_t>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, out_ld, out_off, err);
+                   ? dispatch_vec<float>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, om, err)
+                   : dispatch_vec<uint16_t>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, om, err);
     }
     if (!done) {
         const int64_t total = (int64_t)T_ * B * D;
@@ -168,12 +173,61 @@ int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16
         if (blocks > (int64_t)cus * 16) blocks = (int64_t)cus * 16;
         if (dtype == DLRM_F32)
             hipLaunchKernelGGL(maplookup_scalar<float>, dim3((unsigned)blocks), dim3(256), 0, s, d_tabs, T_, D, idx,
-                               itype, tstride, base, B, L, (float*)out, out_ld, out_off, err);
+                               itype, tstride, base, B, L, (float*)out, om, err);
         else
             hipLaunchKernelGGL(maplookup_scalar<uint16_t>, dim3((unsigned)blocks), dim3(256), 0, s, d_tabs, T_, D, idx,
-                               itype, tstride, base, B, L, (uint16_t*)out, out_ld, out_off, err);
+                               itype, tstride, base, B, L, (uint16_t*)out, om, err);
     }
     return ctx_hip(ctx, hipGetLastError(), "maplookup launch");
+}
+
+// ------------------------------------------------------------------------- row scatter
+// dst + dbase[t] + b * dld[t]  <-  src + b * src_ld + src_off + t * D   (D elements each): the
+// exchange's repack of a [B][T*D] row block into per-destination blocks (sharded.py), one
+// launch for every table.  16-B lanes where the geometry allows.
+// Work item = one 16-B piece (VEC: the source rows are 16-B aligned and D*esize % 16 == 0) or
+// one element.  A destination row that is not 16-B aligned takes the element path.
+template <bool VEC>
+__global__ __launch_bounds__(256) void scatter_rows_kernel(int T_, int B, int D, int esize, const char* __restrict__ src,
+                                                           int64_t src_ld, int64_t src_off, char* __restrict__ dst,
+                                                           const int64_t* __restrict__ dbase,
+                                                           const int64_t* __restrict__ dld) {
+    const int per = VEC ? 16 / esize : 1;  // elements per item
+    const int nv = D / per;
+    const int64_t total = (int64_t)B * T_ * nv;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e % nv);
+        const int64_t bt = e / nv;
+        const int t = (int)(bt % T_);
+        const int64_t b = bt / T_;
+        const int64_t so = (b * src_ld + src_off + (int64_t)t * D + (int64_t)j * per) * esize;
+        const int64_t dof = (dbase[t] + b * dld[t] + (int64_t)j * per) * esize;
+        if (VEC && dof % 16 == 0) {
+            *(uint4*)(dst + dof) = *(const uint4*)(src + so);
+        } else if (esize == 4) {
+            for (int k = 0; k < per; ++k) ((uint32_t*)(dst + dof))[k] = ((const uint32_t*)(src + so))[k];
+        } else {
+            for (int k = 0; k < per; ++k) ((uint16_t*)(dst + dof))[k] = ((const uint16_t*)(src + so))[k];
+        }
+    }
+}
+
+int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T_, int B, int D, const void* src, int64_t src_ld,
+                        int64_t src_off, void* dst, const int64_t* dbase, const int64_t* dld, bool vec_ok) {
+    if (T_ == 0 || B == 0 || D == 0) return DLRM_OK;
+    hipStream_t s = ctx_stream(ctx);
+    const int cus = ctx_num_cus(ctx);
+    const int64_t items = (int64_t)B * T_ * (vec_ok ? D / (16 / esize) : D);
+    int64_t g = (items + 255) / 256;
+    if (g > (int64_t)cus * 16) g = (int64_t)cus * 16;
+    const dim3 grid((unsigned)(g < 1 ? 1 : g));
+    if (vec_ok)
+        hipLaunchKernelGGL(scatter_rows_kernel<true>, grid, dim3(256), 0, s, T_, B, D, esize, (const char*)src, src_ld,
+                           src_off, (char*)dst, dbase, dld);
+    else
+        hipLaunchKernelGGL(scatter_rows_kernel<false>, grid, dim3(256), 0, s, T_, B, D, esize, (const char*)src,
+                           src_ld, src_off, (char*)dst, dbase, dld);
+    return ctx_hip(ctx, hipGetLastError(), "scatter_rows launch");
 }
 
 }  // namespace dlrm

@@ -7,19 +7,21 @@ way moves the looked-up vectors to the ranks that own the samples, and their gra
   rank r owns the tables tables(r) (a TablePartition) and samples [r*B, (r+1)*B) of the
   global batch Bg = world * B (weak scaling: B per GPU is fixed).
 
-  forward : maplookup of r's T_r tables for all Bg samples  -> sbuf [Bg][T_r*D]
-            repack (one copy)                               -> send [world][T_r][B][D]
+  forward : maplookup of r's T_r tables for all Bg samples, written straight into the
+            exchange layout (dlrm_maplookup_blocked)        -> send [world][T_r][B][D]
             all-to-all (block j -> rank j)                  -> recv = [src j][T_j][B][D]
             every table's B vectors for r's samples are now one contiguous [B][D] block of
             recv, i.e. a B-row table whose row b is sample b: the fused lookup+interaction
             kernel runs on these T "received tables" with identity indices (no ys copy)
   backward: dot_back re-gathers T from the received tables (dlrm_interact_bwd_gather)
-            -> dt [B][F*D]; repack dt's table columns in owner order (one copy)
-            all-to-all                                      -> grecv [src i][T_r][B][D]
-            repack (one copy)                               -> grad [Bg][T_r*D]
+            -> dt [B][F*D]; dt's table columns scattered per owner (dlrm_scatter_rows)
+                                                            -> gsend [dst j][B][T_j][D]
+            all-to-all                                      -> grecv [src i][B][T_r][D]
+                                                               = grad [Bg][T_r*D]
             update!(Descent) of r's tables with r's indices for all Bg samples; the
             SparseIndexer (positions grouped by row: a hash build over the whole chip for
-            Bg*L > 4096) is built at the start of the step
+            Bg*L > 4096) depends on the indices only and is built on a side stream while
+            the forward runs
 
 All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-ABI kernels)
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
@@ -118,9 +120,14 @@ class HipShardOps:
         self._ok(self.lib.dlrm_indexer_build(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
                                              idx.itype, idx.stride, self.base, idx.B, idx.L))
 
-    def lookup(self, idx, send):
-        self._ok(self.lib.dlrm_maplookup(self.ctx.bind(), self.ts.handle, ptr(idx.data), idx.itype, idx.stride,
-                                         self.base, idx.B, idx.L, ptr(send), send.stride(0), 0))
+    def lookup_blocked(self, idx, out, ld, tstride, brows, bstride):
+        self._ok(self.lib.dlrm_maplookup_blocked(self.ctx.bind(), self.ts.handle, ptr(idx.data), idx.itype,
+                                                 idx.stride, self.base, idx.B, idx.L, ptr(out), ld, 0, tstride, brows,
+                                                 bstride))
+
+    def scatter_rows(self, src, src_ld, src_off, dst, dbase, dld, T, B, D):
+        self._ok(self.lib.dlrm_scatter_rows(self.ctx.bind(), src.element_size(), T, B, D, ptr(src), src_ld, src_off,
+                                            ptr(dst), ptr(dbase), ptr(dld)))
 
     def interact_fwd_recv(self, x, out, padding):
         i = self.ident
@@ -161,7 +168,6 @@ class ShardedHotPath:
         _, self.width, self.padding = interaction_sizes(dim, self.F)
         dev = device
         D, B, T, Tr, W = dim, batch_local, self.T, self.Tr, self.world
-        self.sbuf = torch.empty((self.Bg, max(Tr, 1) * D), dtype=dtype, device=dev)
         self.send = torch.empty((W * Tr * B * D,), dtype=dtype, device=dev)
         self.recv = torch.empty((T * B * D,), dtype=dtype, device=dev)
         self.out = torch.empty((B, self.width), dtype=dtype, device=dev)
@@ -169,7 +175,7 @@ class ShardedHotPath:
         self.dt = torch.empty((B, self.F * D), dtype=torch.float32, device=dev)
         self.gsend = torch.empty((T * B * D,), dtype=torch.float32, device=dev)
         self.grecv = torch.empty((W * Tr * B * D,), dtype=torch.float32, device=dev)
-        self.grad = torch.empty((self.Bg, max(Tr, 1) * D), dtype=torch.float32, device=dev)
+        self.grad = self.grecv.view(self.Bg, Tr * D) if Tr else None
         # element counts of each peer's block (flat all_to_all_single splits)
         self.fwd_in_splits = [Tr * B * D] * W
         self.fwd_out_splits = [c * B * D for c in partition.counts]
@@ -178,9 +184,17 @@ class ShardedHotPath:
         # received block of global table t: position of t in the exchange order
         slot = {t: i for i, t in enumerate(partition.order)}
         self.recv_tables = [self.recv[slot[t] * B * D:(slot[t] + 1) * B * D].view(B, D) for t in range(T)]
-        self.order = None if partition.order == list(range(T)) else torch.tensor(partition.order, device=dev)
+        # gsend block of owner j = [B][T_j][D]: table t (k-th of its owner) at base + b * T_j * D
+        base, ld, off = [0] * T, [0] * T, 0
+        for j, tabs in enumerate(partition.owners):
+            for k, t in enumerate(tabs):
+                base[t], ld[t] = off + k * D, len(tabs) * D
+            off += len(tabs) * B * D
+        self.gs_base = torch.tensor(base, dtype=torch.int64, device=dev)
+        self.gs_ld = torch.tensor(ld, dtype=torch.int64, device=dev)
         ops.bind_recv(self.recv_tables)
         self._graphs = None
+        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
 
     # ---- exchange (pure data movement; identical for every ShardOps)
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -193,39 +207,29 @@ class ShardedHotPath:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def pack_send(self):
-        """sbuf [Bg][T_r*D] (sample-major) -> send [world][T_r][B][D]."""
-        if self.Tr:
-            W, B, Tr, D = self.world, self.B, self.Tr, self.D
-            self.send.view(W, Tr, B, D).copy_(self.sbuf.view(W, B, Tr, D).permute(0, 2, 1, 3))
-
     def exchange_fwd(self):
         self._a2a(self.recv, self.send, self.fwd_out_splits, self.fwd_in_splits)
 
     def pack_grad(self):
-        """dt's table columns [B][T][D] -> gsend [T][B][D] in exchange order."""
-        B, T, D = self.B, self.T, self.D
-        dt3 = self.dt[:, D:].view(B, T, D).permute(1, 0, 2)
-        if self.order is not None:
-            dt3 = dt3[self.order]
-        self.gsend.view(T, B, D).copy_(dt3)
+        """dt's table columns -> gsend [owner j][B][T_j][D] (one launch)."""
+        self.ops.scatter_rows(self.dt, self.F * self.D, self.D, self.gsend, self.gs_base, self.gs_ld, self.T, self.B,
+                              self.D)
 
     def exchange_bwd(self):
         self._a2a(self.grecv, self.gsend, self.bwd_out_splits, self.bwd_in_splits)
 
-    def unpack_grad(self):
-        """grecv [world][T_r][B][D] -> grad [Bg][T_r*D] (sample-major, as the update reads it)."""
-        if self.Tr:
-            W, B, Tr, D = self.world, self.B, self.Tr, self.D
-            self.grad.view(W, B, Tr, D).copy_(self.grecv.view(W, Tr, B, D).permute(0, 2, 1, 3))
-
     # ---- the step, as three compute segments around the two exchanges
-    def seg_lookup(self, idx):
-        """idx: PackedIndices of this rank's tables for the GLOBAL batch ([T_r][Bg*L])."""
+    def seg_index(self, idx):
+        """The update's SparseIndexer (depends on the indices only)."""
         if self.Tr:
-            self.ops.build_indexer(idx)  # depends on the indices only
-            self.ops.lookup(idx, self.sbuf)
-            self.pack_send()
+            self.ops.build_indexer(idx)
+
+    def seg_lookup(self, idx):
+        """idx: PackedIndices of this rank's tables for the GLOBAL batch ([T_r][Bg*L]);
+        the gathered vectors land in the exchange layout send [world][T_r][B][D]."""
+        if self.Tr:
+            B, D, Tr = self.B, self.D, self.Tr
+            self.ops.lookup_blocked(idx, self.send, D, B * D, B, Tr * B * D)
 
     def seg_interact(self, x, dout):
         self.ops.interact_fwd_recv(x, self.out, self.padding)
@@ -234,10 +238,10 @@ class ShardedHotPath:
 
     def seg_update(self, idx):
         if self.Tr:
-            self.unpack_grad()
             self.ops.update(idx, self.grad, prebuilt=True)
 
     def forward(self, x, idx):
+        self.seg_index(idx)
         self.seg_lookup(idx)
         self.exchange_fwd()
         self.ops.interact_fwd_recv(x, self.out, self.padding)
@@ -251,6 +255,7 @@ class ShardedHotPath:
         return self.dx
 
     def step(self, x, idx, dout):
+        self.seg_index(idx)
         self.seg_lookup(idx)
         self.exchange_fwd()
         self.seg_interact(x, dout)
@@ -260,32 +265,40 @@ class ShardedHotPath:
 
     # ---- hipGraph replay of the compute segments (collectives stay eager)
     def capture(self, x, idx_list, dout):
-        """Captures seg_lookup / seg_update per index batch and seg_interact once."""
-        s = torch.cuda.Stream(device=self.sbuf.device)
+        """Captures seg_index (side stream) / seg_lookup / seg_update per index batch and
+        seg_interact once."""
+        s = torch.cuda.Stream(device=self.send.device)
         s.wait_stream(torch.cuda.current_stream())
-        look, upd = [], []
+        look, upd, ixg = [], [], []
         with torch.cuda.stream(s):
             for idx in idx_list:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
-                    self.seg_lookup(idx)
-                look.append(g)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
-                    self.seg_update(idx)
-                upd.append(g)
+                for lst, fn in ((ixg, self.seg_index), (look, self.seg_lookup), (upd, self.seg_update)):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=s):
+                        fn(idx)
+                    lst.append(g)
             mid = torch.cuda.CUDAGraph()
             with torch.cuda.graph(mid, stream=s):
                 self.seg_interact(x, dout)
         torch.cuda.current_stream().wait_stream(s)
-        self._graphs = (look, mid, upd)
+        self._graphs = (look, mid, upd, ixg)
+        self._ix_done = torch.cuda.Event()
 
     def step_graphed(self, k):
-        look, mid, upd = self._graphs
+        """One step: the indexer build runs on a side stream beside the lookup, the exchanges
+        and the interaction; the update waits for it.  The side stream first waits for the
+        previous step's update (the indexer buffers are reused)."""
+        look, mid, upd, ixg = self._graphs
+        main = torch.cuda.current_stream()
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            ixg[k].replay()
+            self._ix_done.record(self._side)
         look[k].replay()
         self.exchange_fwd()
         mid.replay()
         self.exchange_bwd()
+        main.wait_event(self._ix_done)
         upd[k].replay()
 
 

@@ -107,6 +107,25 @@ int dlrm_maplookup(dlrm_ctx* ctx, const dlrm_tables* tables,
                    int batch, int lookups,
                    void* out, int64_t out_ld, int64_t out_offset);
 
+/* dlrm_maplookup with a general output row map (the table-sharded exchange layout,
+ * dlrm.jl_amd/sharded.py: every peer's block written in place, no repack):
+ *   row b of table t -> out + (b / block_rows) * block_stride + (b % block_rows) * out_ld
+ *                           + out_offset + t * table_stride        (elements)
+ * dlrm_maplookup(...) == dlrm_maplookup_blocked(..., table_stride = dim, block_rows = batch,
+ * block_stride = 0).  No reference counterpart (DLRM.jl is single-process). */
+int dlrm_maplookup_blocked(dlrm_ctx* ctx, const dlrm_tables* tables,
+                           const void* indices, int itype, int64_t table_stride, int index_base,
+                           int batch, int lookups, void* out, int64_t out_ld, int64_t out_offset,
+                           int64_t out_table_stride, int64_t block_rows, int64_t block_stride);
+
+/* Row scatter of the exchange (sharded backward: dt's table columns -> per-owner blocks):
+ *   dst + dst_base[t] + b * dst_ld[t]  <-  src + b * src_ld + src_offset + t * dim
+ * for b < batch, t < num_tables, dim elements of esize (2 or 4) bytes; dst_base / dst_ld are
+ * device arrays of num_tables int64 (elements).  No reference counterpart. */
+int dlrm_scatter_rows(dlrm_ctx* ctx, int esize, int num_tables, int batch, int dim,
+                      const void* src, int64_t src_ld, int64_t src_offset, void* dst,
+                      const int64_t* dst_base, const int64_t* dst_ld);
+
 /* ---- pairwise dot interaction -------------------------------------------------------- */
 /* (dot::DotInteraction)(x, ys): copies x[b][0:d] into ys[b][0:d] (fast_vcat), views
  * ys[b][0:F*d] as T_b = [F][d], and writes

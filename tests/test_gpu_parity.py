@@ -705,3 +705,36 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, gra
         assert np.array_equal(z["dx"], to_np_f32(hp.dx)[sl])
         for t in part.tables(r):
             assert np.array_equal(z[f"t{t}"], to_np_f32(hp.ts[t].data)), (r, t)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_exchange_layout_kernels(pkg, gpu, dtype):
+    """dlrm_maplookup_blocked (lookup written straight into the [peer][table][b][D] send layout)
+    == maplookup + the permute; dlrm_scatter_rows == the per-owner column scatter, bit for bit
+    (16-B and element paths)."""
+    from dlrm_jl_amd.sharded import HipShardOps
+    rng = np.random.default_rng(21)
+    rows, D, L, W, Bl = [10, 300, 5000], 32, 2, 3, 16
+    T, Bg = len(rows), W * Bl
+    tabs = rand_tables(rng, rows, D)
+    idx = torch.from_numpy(rand_indices(rng, rows, Bg, L)).to(torch.int32).reshape(T, Bg, L).to(gpu)
+    ops = HipShardOps(dev_tables(tabs, gpu, dtype), Bg, L, 0.1, device=gpu)
+    p = pkg.PackedIndices(idx)
+    ref = pkg.maplookup(pkg.PreallocationStrategy(0), ops.ts, p, index_base=0)
+    out = torch.zeros(W * T * Bl * D, dtype=dtype, device=gpu)
+    ops.lookup_blocked(p, out, D, Bl * D, Bl, T * Bl * D)
+    want = ref.reshape(W, Bl, T, D).permute(0, 2, 1, 3).reshape(-1)
+    assert np.array_equal(to_np_bits(out), to_np_bits(want))
+    # scatter: owners [[2, 0], [1]] -> per-owner [B][T_j][D] blocks, plus an odd (unaligned) layout
+    B, F = 24, T + 1
+    src = torch.from_numpy(rng.standard_normal((B, F * D)).astype(np.float32)).to(gpu)
+    for base, ld in (([D, 2 * B * D, 0], [2 * D, D, 2 * D]), ([1, 2 * B * D + 5, D + 2], [2 * D + 3, D, 2 * D + 3])):
+        n = 4 * B * D + 64
+        dst = torch.zeros(n, dtype=torch.float32, device=gpu)
+        ops.scatter_rows(src, F * D, D, dst, torch.tensor(base, device=gpu), torch.tensor(ld, device=gpu), T, B, D)
+        exp = np.zeros(n, dtype=np.float32)
+        s_np = src.cpu().numpy()
+        for b in range(B):
+            for t in range(T):
+                exp[base[t] + b * ld[t]: base[t] + b * ld[t] + D] = s_np[b, D + t * D: D + (t + 1) * D]
+        assert np.array_equal(dst.cpu().numpy(), exp)

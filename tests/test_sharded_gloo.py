@@ -40,8 +40,23 @@ class OracleShardOps:
     def build_indexer(self, idx):
         pass
 
-    def lookup(self, idx, send):
-        self.o.maplookup(self.tables, idx.data.numpy().astype(np.int64), 0, idx.B, idx.L, send.numpy(), 0)
+    def lookup_blocked(self, idx, out, ld, tstride, brows, bstride):
+        T, Bg, D = len(self.tables), idx.B, self.tables[0].shape[1]
+        tmp = np.zeros((Bg, T * D), dtype=np.float32)
+        self.o.maplookup(self.tables, idx.data.numpy().astype(np.int64), 0, Bg, idx.L, tmp, 0)
+        b = np.arange(Bg)[:, None, None]
+        t = np.arange(T)[None, :, None]
+        c = np.arange(D)[None, None, :]
+        dst = (b // brows) * bstride + (b % brows) * ld + t * tstride + c
+        out.view(-1).numpy()[dst.reshape(-1)] = tmp.reshape(-1)
+
+    def scatter_rows(self, src, src_ld, src_off, dst, dbase, dld, T, B, D):
+        b = np.arange(B)[:, None, None]
+        t = np.arange(T)[None, :, None]
+        c = np.arange(D)[None, None, :]
+        s_ = (b * src_ld + src_off + t * D + c).reshape(-1)
+        d_ = (dbase.numpy()[None, :, None] + b * dld.numpy()[None, :, None] + c).reshape(-1)
+        dst.view(-1).numpy()[d_] = src.reshape(-1).numpy()[s_]
 
     def _ys(self, x):
         return torch.cat([x] + list(self.recv_tables), dim=1).numpy()
