@@ -108,8 +108,8 @@ def make_inputs(pkg, w, B, dev, rank, T_rows):
     tables = []
     for n in T_rows:
         s = 1.0 / float(np.sqrt(n))
-        t = torch.empty((n, D), dtype=torch.float32, device=dev).uniform_(-s, s, generator=g)
-        tables.append(t.to(dt) if dt != torch.float32 else t)
+        # drawn in the table dtype directly (a 293M-row Terabyte table has no room for an fp32 copy)
+        tables.append(torch.empty((n, D), dtype=dt, device=dev).uniform_(-s, s, generator=g))
     idx = []
     zipf = w.get("zipf")
     rng = np.random.default_rng(51234 + rank)

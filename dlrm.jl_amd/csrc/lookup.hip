@@ -17,7 +17,10 @@
 
 namespace dlrm {
 
-template <typename T, int VPR, int U>
+// KB lookups of a bag are fetched per round: their indices first (independent loads), then
+// U x KB rows in flight, then accumulated in k order -- a pooled bag costs ceil(L / KB)
+// index->row round trips instead of L.
+template <typename T, int VPR, int U, int KB>
 __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict__ tabs, int ntab,
                                                      const void* __restrict__ idx, int itype,
                                                      int64_t tstride, int base, int B, int L,
@@ -36,51 +39,59 @@ __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict
     constexpr int D = VPR * NE;
 
     for (int64_t first = wave * (RPW * U); first < total; first += nwaves * (RPW * U)) {
-        int64_t item[U];
-        const T* rowp[U];
+        int64_t bb[U];
+        int tt[U];
         bool live[U];
         float acc[U][VPL][NE];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            item[u] = first + u * RPW + g;
-            live[u] = item[u] < total;
+            const int64_t item = first + u * RPW + g;
+            live[u] = item < total;
+            bb[u] = item / ntab;
+            tt[u] = (int)(item - bb[u] * ntab);
         }
-        for (int k = 0; k < L; ++k) {
-            typename V::type vv[U][VPL];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                rowp[u] = nullptr;
-                if (live[u]) {
-                    const int64_t b = item[u] / ntab;
-                    const int t = (int)(item[u] - b * ntab);
-                    const int64_t r = load_index(idx, itype, t * tstride + b * L + k) - base;
-                    if (r >= 0 && r < tabs[t].nrows) rowp[u] = (const T*)tabs[t].data + r * D;
-                    else if (v == 0) raise_index_error(err);
-                }
-            }
+        for (int k0 = 0; k0 < L; k0 += KB) {
+            int64_t r[U][KB];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int j = 0; j < VPL; ++j) {
-                    if (rowp[u]) vv[u][j] = *((const typename V::type*)(rowp[u]) + v + j * 64);
-                    else vv[u][j] = typename V::type{};
+                for (int kk = 0; kk < KB; ++kk)
+                    r[u][kk] = load_index_if(live[u] && k0 + kk < L, idx, itype,
+                                             tt[u] * tstride + bb[u] * L + k0 + kk) - base;
+            typename V::type vv[U][KB][VPL];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int kk = 0; kk < KB; ++kk) {
+                    const T* rowp = nullptr;
+                    if (live[u] && k0 + kk < L) {
+                        if (r[u][kk] >= 0 && r[u][kk] < tabs[tt[u]].nrows) rowp = (const T*)tabs[tt[u]].data + r[u][kk] * D;
+                        else if (v == 0) raise_index_error(err);
+                    }
+#pragma unroll
+                    for (int j = 0; j < VPL; ++j) {
+                        if (rowp) vv[u][kk][j] = *((const typename V::type*)(rowp) + v + j * 64);
+                        else vv[u][kk][j] = typename V::type{};
+                    }
                 }
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int j = 0; j < VPL; ++j) {
-                    float f[NE];
-                    V::to_f32(vv[u][j], f);
+                for (int kk = 0; kk < KB; ++kk) {
+                    if (k0 + kk >= L) break;
 #pragma unroll
-                    for (int e = 0; e < NE; ++e) acc[u][j][e] = (k == 0) ? f[e] : acc[u][j][e] + f[e];
+                    for (int j = 0; j < VPL; ++j) {
+                        float f[NE];
+                        V::to_f32(vv[u][kk][j], f);
+#pragma unroll
+                        for (int e = 0; e < NE; ++e) acc[u][j][e] = (k0 + kk == 0) ? f[e] : acc[u][j][e] + f[e];
+                    }
                 }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (!live[u]) continue;
-            const int64_t b = item[u] / ntab;
-            const int t = (int)(item[u] - b * ntab);
-            T* o = out + om.row(b) + (int64_t)t * om.tstride;
+            T* o = out + om.row(bb[u]) + (int64_t)tt[u] * om.tstride;
 #pragma unroll
             for (int j = 0; j < VPL; ++j) *((typename V::type*)o + v + j * 64) = V::from_f32(acc[u][j]);
         }
@@ -117,15 +128,19 @@ static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, int T_, co
                        int64_t tstride, int base, int B, int L, void* out, const OutMap& om, unsigned* err) {
     constexpr int LPR = VPR <= 64 ? VPR : 64;
     constexpr int RPW = 64 / LPR;
-    constexpr int U = 4;
+    const int U = L > 1 ? 2 : 4;  // pooled: 2 bags x 4 lookups in flight per lane group
     const int64_t total = (int64_t)T_ * B;
     const int64_t waves = (total + RPW * U - 1) / (RPW * U);
     int64_t blocks = (waves + 3) / 4;
     const int64_t cap = (int64_t)cus * 16;  // grid-stride beyond 16 blocks per CU
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL((maplookup_vec<T, VPR, U>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx, itype,
-                       tstride, base, B, L, (T*)out, om, err);
+    if (L > 1)
+        hipLaunchKernelGGL((maplookup_vec<T, VPR, 2, 4>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx,
+                           itype, tstride, base, B, L, (T*)out, om, err);
+    else
+        hipLaunchKernelGGL((maplookup_vec<T, VPR, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx,
+                           itype, tstride, base, B, L, (T*)out, om, err);
 }
 
 template <typename T>

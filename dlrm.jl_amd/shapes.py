@@ -27,8 +27,15 @@ WORKLOADS = {
     "kaggle-d128-b2048": dict(rows=KAGGLE_EMBEDDING_SIZES, dim=128, batch=2048, lookups=1, dtype="f32"),
     # configs[2]: 26 tables, dim 128, batch 8192, bf16 — MFMA interaction
     "kaggle-d128-b8192-bf16": dict(rows=KAGGLE_EMBEDDING_SIZES, dim=128, batch=8192, lookups=1, dtype="bf16"),
+    # configs[3]: Criteo-Terabyte rows (882.8M, Zipf).  fp32 (452 GB) needs >= 2 GPUs (table-sharded,
+    # TablePartition.fitting); bf16 (226 GB) fits one MI355X's 288 GB
+    "terabyte-d128-zipf": dict(rows=TERABYTE_EMBEDDING_SIZES, dim=128, batch=2048, lookups=1, dtype="f32", zipf=1.05,
+                               rows_src="Criteo-Terabyte (criteo.jl:379-406)"),
+    "terabyte-d128-bf16-zipf": dict(rows=TERABYTE_EMBEDDING_SIZES, dim=128, batch=2048, lookups=1, dtype="bf16",
+                                    zipf=1.05, rows_src="Criteo-Terabyte (criteo.jl:379-406)"),
     # configs[4]: pooled mode, 64 tables x dim 256, hot-row skew (rows per table: 1M)
-    "pooled-64x256-l10": dict(rows=[1_000_000] * 64, dim=256, batch=2048, lookups=10, dtype="f32", zipf=1.2),
+    "pooled-64x256-l10": dict(rows=[1_000_000] * 64, dim=256, batch=2048, lookups=10, dtype="f32", zipf=1.2,
+                              rows_src="64 x 1M synthetic"),
 }
 
 

@@ -728,7 +728,7 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
     # scatter: owners [[2, 0], [1]] -> per-owner [B][T_j][D] blocks, plus an odd (unaligned) layout
     B, F = 24, T + 1
     src = torch.from_numpy(rng.standard_normal((B, F * D)).astype(np.float32)).to(gpu)
-    for base, ld in (([D, 2 * B * D, 0], [2 * D, D, 2 * D]), ([1, 2 * B * D + 5, D + 2], [2 * D + 3, D, 2 * D + 3])):
+    for base, ld in (([D, 2 * B * D, 0], [2 * D, D, 2 * D]), ([1, 3 * B * D + 5, D + 2], [2 * D + 3, D, 2 * D + 3])):
         n = 4 * B * D + 64
         dst = torch.zeros(n, dtype=torch.float32, device=gpu)
         ops.scatter_rows(src, F * D, D, dst, torch.tensor(base, device=gpu), torch.tensor(ld, device=gpu), T, B, D)
