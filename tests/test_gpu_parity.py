@@ -447,7 +447,8 @@ def _dt_written_mask(idx, D):
     ([300, 100000, 3, 5_000_000], 64, 6000, 1.1, torch.float32),       # N > 4096: split hash build
     ([5, 100000, 3, 77] * 6 + [9, 10], 128, 8192, None, torch.bfloat16),  # configs[2] shape (bf16, B=8192)
     ([50] * 40, 32, 200, None, torch.float32),                         # F = 41: unsplit fallback
-    ([1], 16, 64, None, torch.float32)])                               # every position hits one row
+    ([1], 16, 64, None, torch.float32),                                # every position hits one row
+    ([10, 3000, 7, 100000, 3], 256, 512, 1.2, torch.float32)])         # 1-KB rows: 4 chunks per lane group
 def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
     """dlrm_step_fwd / dlrm_step_bwd (indexer built in the forward's launch, once-hit rows
     updated inside the backward) == maplookup -> DotInteraction -> dot_back -> update!
