@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
-    ap.add_argument("--overlap-indexer", type=int, default=0)
+    ap.add_argument("--overlap-indexer", type=int, default=-1, help="-1: the engine's default")
     ap.add_argument("--fused", type=int, default=1)
     ap.add_argument("--materialize-ys", type=int, default=-1,
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
@@ -207,7 +207,8 @@ def main():
     if world == 1:
         tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows)
         ts = pkg.EmbeddingTableSet(tables)
-        engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0, overlap_indexer=bool(a.overlap_indexer),
+        engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0,
+                             overlap_indexer=None if a.overlap_indexer < 0 else bool(a.overlap_indexer),
                              fused=bool(a.fused),
                              materialize_ys=None if a.materialize_ys < 0 else bool(a.materialize_ys))
         F = T + 1

@@ -18,6 +18,10 @@ using namespace dlrm;
 struct dlrm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // side stream + fork/join events: work that depends only on the indices (the hash indexer
+    // build) runs beside the forward; graph capture follows the fork and the join
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     unsigned* err = nullptr;  // device error word
     int cus = 256;
     char msg[512] = {0};
@@ -89,6 +93,14 @@ static bool built_from(const dlrm_indexer* ix, const void* indices, int itype, i
            ix->tstride == tstride && ix->base == base;
 }
 
+static int ensure_side(dlrm_ctx* ctx) {
+    if (ctx->side) return DLRM_OK;
+    int rc = ctx_hip(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking), "hipStreamCreate(side)");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "hipEventCreate");
+    return rc;
+}
+
 extern "C" {
 
 int dlrm_abi_version(void) { return DLRM_HIP_ABI_VERSION; }
@@ -119,6 +131,9 @@ int dlrm_ctx_create(int device, void* stream, dlrm_ctx** out) {
 
 int dlrm_ctx_destroy(dlrm_ctx* ctx) {
     if (!ctx) return DLRM_OK;
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->err) (void)hipFree(ctx->err);
     delete ctx;
     return DLRM_OK;
@@ -546,6 +561,29 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         return DLRM_OK;
     }
     if (rc != DLRM_E_UNSUPPORTED) return rc;
+    if (ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
+        // large batch: the hash build in its split form (once-hit rows left to dlrm_step_bwd), on
+        // the side stream beside the fused forward (launched below); the main stream joins it
+        rc = ensure_side(ctx);
+        if (rc) return rc;
+        rc = ctx_hip(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "hipEventRecord(fork)");
+        if (rc == DLRM_OK) rc = ctx_hip(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0), "hipStreamWaitEvent(side)");
+        if (rc == DLRM_OK)
+            rc = launch_hix_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
+                                  true, ctx->side);
+        if (rc == DLRM_OK) rc = ctx_hip(ctx, hipEventRecord(ctx->ev_join, ctx->side), "hipEventRecord(join)");
+        if (rc) return rc;
+        rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype,
+                                        table_stride, index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld,
+                                        padding);
+        const int rj = ctx_hip(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0), "hipStreamWaitEvent(main)");
+        if (rc == DLRM_E_UNSUPPORTED)
+            return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
+                            "dlrm_step_fwd: no fused forward for this shape (16-B aligned rows and x, F <= 96 needed)");
+        if (rc || rj) return rc ? rc : rj;
+        record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+        return DLRM_OK;
+    }
     // no single-launch form for this shape: the fused forward, then the (unsplit) indexer
     rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                     index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding);
@@ -553,13 +591,6 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
                         "dlrm_step_fwd: no fused forward for this shape (16-B aligned rows and x, F <= 96 needed)");
     if (rc) return rc;
-    if (ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
-        // large batch: the hash build in its split form (once-hit rows left to dlrm_step_bwd)
-        rc = launch_hix_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, true);
-        if (rc) return rc;
-        record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
-        return DLRM_OK;
-    }
     return dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, 1);
 }
 

@@ -333,16 +333,16 @@ int64_t hix_table_slots(int64_t cap) {
 }
 
 int launch_hix_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx, int itype,
-                     int64_t tstride, int base, int N, bool split) {
+                     int64_t tstride, int base, int N, bool split, hipStream_t stream) {
+    hipStream_t s = stream ? stream : ctx_stream(ctx);
     if (T_ == 0 || N == 0) {
         // empty batch: every table reports zero segments
-        if (T_) return ctx_hip(ctx, hipMemsetAsync(ix.counts, 0, sizeof(int32_t) * 8 * T_, ctx_stream(ctx)), "memset");
+        if (T_) return ctx_hip(ctx, hipMemsetAsync(ix.counts, 0, sizeof(int32_t) * 8 * T_, s), "memset");
         return DLRM_OK;
     }
     if (!ix.hsize || N > kHixMaxN || (int64_t)N > ix.cap)
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "hash indexer: N=%d (cap %lld, hash slots %lld)", N,
                         (long long)ix.cap, (long long)ix.hsize);
-    hipStream_t s = ctx_stream(ctx);
     const dim3 gp((N + kHixTile - 1) / kHixTile, T_), gs((unsigned)(ix.hsize / (256 * kHixSPT)), T_);
     hipLaunchKernelGGL(hix_insert_kernel, gp, dim3(256), 0, s, ix, tabs, idx, itype, tstride, base, N,
                        ctx_error_word(ctx));

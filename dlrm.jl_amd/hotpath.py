@@ -14,8 +14,9 @@ All buffers are allocated once; a step issues 3 kernel launches on the current s
 bwd with the SGD step of once-hit rows, then the apply of repeated rows) with no host
 synchronisation, so the whole step can be captured in a torch.cuda graph (`fused=False`
 runs maplookup and the interaction as two launches, like the reference).  With
-`overlap_indexer=True` the indexer sort (which depends only on the indices) runs on a side
-stream concurrently with the lookup and the interaction.
+`overlap_indexer=True` (the default where ys is kept and the indexer is the hash build,
+B*L > 4096) the indexer (which depends only on the indices) runs on a side stream
+concurrently with the lookup and the interaction.
 
 `materialize_ys` (default: off wherever it applies, i.e. fused forward and one-hot lookups):
 the reference keeps the lookup output ys (= the interaction's T) for dot_back.  Off, the
@@ -35,7 +36,7 @@ from .update import SparseIndexer
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=False, pad_to=1, fused=True, materialize_ys=None):
+                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -62,7 +63,11 @@ class HotPath:
         self.ctx = self.ts.ctx
         self.lib = self.ctx.lib
         self.dcode = dtype_code(dt)
-        self.overlap_indexer = overlap_indexer and deterministic
+        if overlap_indexer is None:
+            # default: a hash-built indexer (B*L > 4096 positions per table) of the operator path
+            # runs on a side stream beside the forward (the step API forks it inside dlrm_step_fwd)
+            overlap_indexer = self.materialize_ys and self.B * self.L > 4096
+        self.overlap_indexer = bool(overlap_indexer) and deterministic
         self._side = torch.cuda.Stream(device=dev) if self.overlap_indexer else None
         self._indexer_done = None
         # the training-step pair (dlrm_step_fwd / dlrm_step_bwd): indexer built inside the forward's
