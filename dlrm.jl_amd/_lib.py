@@ -60,6 +60,7 @@ SIGNATURES = {
     "dlrm_maplookup": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _i64]),
     "dlrm_maplookup_blocked": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _i64,
                                       _i64]),
+    "dlrm_indexer_build_split": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32]),
     "dlrm_scatter_rows": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp, _vp, _vp]),
     "dlrm_interact_fwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_lookup_interact_fwd": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64,

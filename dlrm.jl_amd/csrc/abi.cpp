@@ -456,6 +456,22 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
     return DLRM_OK;
 }
 
+int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, const void* indices, int itype,
+                             int64_t table_stride, int index_base, int batch) {
+    CHECK_ARG(ctx && ix && tb, "dlrm_indexer_build_split: null argument");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    CHECK_ARG(tb->T == ix->T, "dlrm_indexer_build_split: indexer has %d tables, tables has %d", ix->T, tb->T);
+    CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_build_split: batch %d > capacity %lld", batch,
+              (long long)ix->dev.cap);
+    ix->built = false;
+    rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, 1,
+                              true, nullptr);
+    if (rc) return rc;
+    record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+    return DLRM_OK;
+}
+
 int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t* num_unique, int64_t* rows,
                       int64_t* positions, int64_t* seg_start, int64_t cap) {
     CHECK_ARG(ctx && ix && num_unique, "dlrm_indexer_read: null argument");

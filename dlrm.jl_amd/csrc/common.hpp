@@ -225,7 +225,8 @@ int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_align
 int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const void* src, int64_t src_ld,
                         int64_t src_off, void* dst, const int64_t* dbase, const int64_t* dld, bool vec_ok);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
-                         int itype, int64_t tstride, int base, int B, int L);
+                         int itype, int64_t tstride, int base, int B, int L, bool split = false,
+                         hipStream_t stream = nullptr);
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
                      float lr);

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kBuildThreads) void indexer_build_kernel(
 #endif
 }
 
-template <int NT, int EPL>
+template <int NT, int EPL, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const TableDesc* __restrict__ tabs,
                                                           const void* __restrict__ idx, int itype, int64_t tstride,
                                                           int base, int N, unsigned* __restrict__ err) {
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
     if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
 #endif
     PHASE(0);
-    fast_index_table<NT, EPL>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
+    fast_index_table<NT, EPL, SPLIT>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
 #endif
@@ -624,32 +624,42 @@ __global__ __launch_bounds__(256) void sgd_atomic_kernel(TableDesc* __restrict__
 // ------------------------------------------------------------------------ launchers
 size_t indexer_lds_bytes() { return sizeof(uint32_t) * 2 * kLdsSortMax + sizeof(int32_t) * 2 * kLdsSortMax; }
 
+template <int NT, int EPL, bool SPLIT>
+static void launch_fast(hipStream_t s, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx, int itype,
+                        int64_t tstride, int base, int N, unsigned* err) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)indexer_fast_kernel<NT, EPL, SPLIT>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(FastLds<NT, EPL>));
+    (void)attr;
+    hipLaunchKernelGGL((indexer_fast_kernel<NT, EPL, SPLIT>), dim3(T_), dim3(NT), sizeof(FastLds<NT, EPL>), s, ix, tabs,
+                       idx, itype, tstride, base, N, err);
+}
+
+// split: the form dlrm_step_bwd consumes (once-hit positions flagged, their rows left to the
+// backward).  stream: NULL = the context's stream.
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx,
-                         int itype, int64_t tstride, int base, int B, int L) {
+                         int itype, int64_t tstride, int base, int B, int L, bool split, hipStream_t stream) {
     if (T_ == 0) return DLRM_OK;
-    hipStream_t s = ctx_stream(ctx);
+    hipStream_t s = stream ? stream : ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
+    unsigned* err = ctx_error_word(ctx);
     static const bool ix256 = getenv("DLRM_IX256") != nullptr;  // experiment knob
-    if (ix256 && N <= 2048) {  // the 256-thread form the forward / backward launches use, on its own
-        hipLaunchKernelGGL((indexer_fast_kernel<256, 8>), dim3(T_), dim3(256), sizeof(FastLds<256, 8>), s, ix, tabs,
-                           idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
-        return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
-    }
-    if (N <= 1024 * 2) {
-        hipLaunchKernelGGL((indexer_fast_kernel<1024, 2>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 2>), s, ix, tabs,
-                           idx, itype, tstride, base, (int)N, ctx_error_word(ctx));
+    if (ix256 && N <= 2048 && !split) {  // the 256-thread form the forward / backward launches use, on its own
+        launch_fast<256, 8, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
+    } else if (N <= 1024 * 2) {
+        if (split) launch_fast<1024, 2, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
+        else launch_fast<1024, 2, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
     } else if (N <= kFastMaxN) {
-        static const hipError_t a4 = hipFuncSetAttribute((const void*)indexer_fast_kernel<1024, 4>,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                         (int)sizeof(FastLds<1024, 4>));
-        (void)a4;
-        hipLaunchKernelGGL((indexer_fast_kernel<1024, 4>), dim3(T_), dim3(1024), sizeof(FastLds<1024, 4>), s, ix, tabs, idx,
-                           itype, tstride, base, (int)N, ctx_error_word(ctx));
+        if (split) launch_fast<1024, 4, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
+        else launch_fast<1024, 4, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
     } else if (ix.hsize && N <= kHixMaxN) {
-        return launch_hix_build(ctx, ix, tabs, T_, idx, itype, tstride, base, (int)N, false);
-    } else
+        return launch_hix_build(ctx, ix, tabs, T_, idx, itype, tstride, base, (int)N, split, s);
+    } else if (split) {
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "split indexer build: %lld positions per table", (long long)N);
+    } else {
         hipLaunchKernelGGL(indexer_build_kernel<false>, dim3(T_), dim3(kBuildThreads), 0, s, ix, tabs, idx, itype,
-                           tstride, base, B, L, ctx_error_word(ctx));
+                           tstride, base, B, L, err);
+    }
     return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
 }
 

@@ -36,7 +36,7 @@ from .update import SparseIndexer
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None):
+                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None, pipeline=False):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -73,6 +73,16 @@ class HotPath:
         # the training-step pair (dlrm_step_fwd / dlrm_step_bwd): indexer built inside the forward's
         # launch, once-hit rows updated inside the backward's, the rest by the apply launch
         self.step_api = (not self.materialize_ys) and self.indexer is not None and not self.overlap_indexer
+        # pipelined steps (`step_next`): the NEXT batch's split indexer is built on a side stream
+        # during this step, so the step's own launches are the forward (no indexer workgroups),
+        # the backward and the apply; two indexers alternate
+        self.pipeline = bool(pipeline) and self.step_api and self.L == 1
+        if self.pipeline:
+            self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
+            self._ix_of = [None, None]  # the PackedIndices each indexer was last built from
+            self._cur = 0
+            self._pside = torch.cuda.Stream(device=dev)
+            self._pev = torch.cuda.Event()
 
     # -- pieces --------------------------------------------------------------------------
     def _check(self, rc):
@@ -150,6 +160,39 @@ class HotPath:
                                            idx.stride, self.index_base, self.B, ptr(x), x.stride(0), ptr(dout),
                                            dout.stride(0), self.padding, ptr(self.dx), self.dx.stride(0),
                                            ptr(self.dt), self.dt.stride(0), self.lr, flags))
+
+    def build_split(self, indexer, idx):
+        """dlrm_indexer_build_split: the indexer form dlrm_step_bwd consumes."""
+        h = self.ctx.bind()
+        self._check(self.lib.dlrm_indexer_build_split(h, indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
+                                                      idx.stride, self.index_base, self.B))
+
+    def prime(self, idx):
+        """Builds the indexer of the batch the next `step_next` call will process."""
+        self.build_split(self._ixs[self._cur], idx)
+        self._ix_of[self._cur] = idx
+
+    def step_next(self, x, idx, dout, next_idx):
+        """One training step of batch `idx` (same math as `step`, bit for bit) that also builds
+        batch `next_idx`'s indexer on a side stream: exactly one indexer build per step, off the
+        step's critical path (it depends only on the indices).  The side stream first waits for
+        everything queued so far (the previous step's apply read the buffer it rebuilds) and is
+        joined at the end of the step."""
+        cur, nxt = self._cur, 1 - self._cur
+        if self._ix_of[cur] is not idx:  # out of sequence (first call, or a different batch)
+            self.prime(idx)
+        main = torch.cuda.current_stream(self.ts.device)
+        self._pside.wait_stream(main)
+        with torch.cuda.stream(self._pside):
+            self.build_split(self._ixs[nxt], next_idx)
+            self._pev.record(self._pside)
+        self._ix_of[nxt] = next_idx
+        self.lookup_interact_fwd(x, idx)  # ys not materialized: the fused forward alone
+        self.indexer = self._ixs[cur]
+        self.step_bwd(dout, x=x, idx=idx)
+        main.wait_event(self._pev)
+        self._cur = nxt
+        return self.dx
 
     # -- step --------------------------------------------------------------------------
     def validate(self, x, idx, dout=None):

@@ -177,6 +177,15 @@ int dlrm_indexer_destroy(dlrm_indexer* indexer);
 int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
                        const void* indices, int itype, int64_t table_stride, int index_base,
                        int batch, int lookups);
+/* The split form of the indexer that dlrm_step_bwd consumes (one-hot batches): positions whose
+ * row is hit once are flagged (dlrm_step_bwd updates those rows inside the backward), the other
+ * rows are listed for the apply.  dlrm_step_fwd builds it inside the forward's launch; building
+ * it here instead lets a caller prepare the NEXT batch's indexer ahead of time (it depends only
+ * on the indices, e.g. on a side stream during the current step) and run a step as
+ * dlrm_lookup_interact_fwd(ys = NULL) + dlrm_step_bwd. */
+int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
+                             const void* indices, int itype, int64_t table_stride, int index_base,
+                             int batch);
 /* Inspection (synchronous): unique-row count of one table; if rows != NULL copies up to
  * cap unique rows (0-based, in segment order); if positions != NULL copies up to cap
  * positions (b*lookups + k) grouped by segment and the segment starts (cap+1 entries). */

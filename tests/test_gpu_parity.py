@@ -739,3 +739,49 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
             for t in range(T):
                 exp[base[t] + b * ld[t]: base[t] + b * ld[t] + D] = s_np[b, D + t * D: D + (t + 1) * D]
         assert np.array_equal(dst.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("rows,D,B,dtype", [("kaggle", 128, 2048, torch.float32),
+                                            ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32),
+                                            ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16)])
+def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype):
+    """HotPath.step_next (the next batch's split indexer built on a side stream during the
+    step; eager steps, then hipGraph-captured ones) == the operator sequence over the same
+    batches, bit for bit."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    rng = np.random.default_rng(B + 7)
+    T = len(rows)
+    tabs = [rng.uniform(-1, 1, size=(n, D)).astype(np.float32) for n in rows]
+    packs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1, zipf=1.1)).to(torch.int32).to(gpu))
+             for _ in range(3)]
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu).to(dtype)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0, pipeline=True)
+    assert hp.pipeline
+    order = [0, 1, 2, 0]
+    hp.step_next(x, packs[0], dout, packs[1])
+    hp.step_next(x, packs[1], dout, packs[2])
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            hp.step_next(x, packs[2], dout, packs[0])
+            hp.step_next(x, packs[0], dout, packs[1])
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    ts2 = pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype))
+    for k in order:
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts2, packs[k], index_base=0)
+        out, back = pkg.rrule(pkg.DotInteraction(), x, ys)
+        _, dx, dy = back(dout)
+        pkg.update_(pkg.Descent(0.5), ts2, pkg.maplookup_pullback(D, ts2, packs[k], dy), index_base=0)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_bits(hp.out), to_np_bits(out))
+    assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
+    for a, b in zip(hp.ts, ts2):
+        assert np.array_equal(to_np_bits(a.data), to_np_bits(b.data))
