@@ -577,7 +577,23 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         return DLRM_OK;
     }
     if (rc != DLRM_E_UNSUPPORTED) return rc;
-    if (ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
+    const bool split_ok = step_split_supported(tb->aligned16, tb->T, tb->dtype, d, x, x_ld);
+    if (split_ok && batch <= kFastMaxN) {
+        // no single-launch form for this shape (B > 2048): the fused forward, then the split
+        // indexer in LDS (one 1024-thread workgroup per table)
+        rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype,
+                                        table_stride, index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld,
+                                        padding);
+        if (rc == DLRM_OK)
+            rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base,
+                                      batch, 1, true, nullptr);
+        if (rc == DLRM_OK) {
+            record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+            return DLRM_OK;
+        }
+        if (rc != DLRM_E_UNSUPPORTED) return rc;
+    }
+    if (split_ok && ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
         // large batch: the hash build in its split form (once-hit rows left to dlrm_step_bwd), on
         // the side stream beside the fused forward (launched below); the main stream joins it
         rc = ensure_side(ctx);

@@ -219,6 +219,7 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int64_t hix_table_slots(int64_t cap);
 int launch_hix_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
                      int64_t tstride, int base, int N, bool split, hipStream_t stream = nullptr);
+bool step_split_supported(bool tabs_aligned16, int T, int dtype, int d, const void* x, int64_t x_ld);
 int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                          const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
                          const OutMap& om);

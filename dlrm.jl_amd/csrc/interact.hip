@@ -827,6 +827,13 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
                                   tabs_aligned16, x, x_ld);
 }
 
+// Shapes whose backward can take a split indexer (interact_bwd_update_kernel: F <= 32, 16-B
+// aligned rows and x), whatever the batch size.
+bool step_split_supported(bool tabs_aligned16, int T_, int dtype, int d, const void* x, int64_t x_ld) {
+    const int NB = (T_ + 1 + 15) / 16;
+    return T_ > 0 && tabs_aligned16 && fwd_aligned(dtype, d, x, x_ld, nullptr, 0) && NB <= 2;
+}
+
 // Training-step forward (split indexer in the same grid).  DLRM_E_UNSUPPORTED when the shape
 // has no such kernel (the caller then runs the fused forward and the indexer separately).
 int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype, const void* idx,

@@ -212,7 +212,8 @@ def _np_segments(idx_row):
                                            ([1_000_000, 1_000_000, 3], 2048, 10, 1.2),
                                            ([2, 100000, 33_000_000], 16384, 1, None),
                                            ([5000], 4097, 1, 1.05), ([1], 6000, 1, None),
-                                           ([64] * 3, 300, 20, None)])
+                                           ([64] * 3, 300, 20, None), ([3, 70000, 1000], 8193, 1, 1.1),
+                                           ([2, 100000, 33_000_000], 8192, 1, None)])
 def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
     """Both sort strategies (1 pass + bucket rank; full LSD radix on skewed rows), LDS and
     global-scratch variants: unique rows and per-row positions must match numpy exactly."""
@@ -323,10 +324,12 @@ def test_sgd_update_hash_build_vs_oracle(pkg, gpu, rows, B, L, zipf):
         assert np.array_equal(new[untouched], tabs[t][untouched])
 
 
-def test_hash_build_bounds_error_and_reuse(pkg, gpu):
-    """Large-N build: an out-of-range index is skipped and flagged; the next build with the
-    same indexer (slots reset by the previous build) is exact again."""
-    rows, B = [10, 50000], 6000
+@pytest.mark.parametrize("B", [6000, 9000])
+def test_hash_build_bounds_error_and_reuse(pkg, gpu, B):
+    """Large-N builds (the hash build beyond 4096 positions): an out-of-range index is
+    skipped and flagged; the next build with the same indexer (hash slots reset by the
+    previous build) is exact again."""
+    rows = [10, 50000]
     rng = np.random.default_rng(11)
     idx = rand_indices(rng, rows, B, 1)
     bad = idx.copy()
@@ -444,9 +447,11 @@ def _dt_written_mask(idx, D):
     ([3, 4, 10, 1000, 5_000_000], 128, 2048, 1.1, torch.float32),      # hot rows (multi-slice segments)
     ([5, 100000, 3, 77] * 6 + [9, 10], 128, 300, None, torch.bfloat16),
     ([300, 100000, 5_000_000], 64, 3000, None, torch.float32),         # N > 2048: unsplit fallback
+    ([300, 100000, 3, 5_000_000], 64, 3000, 1.1, torch.float32),       # 2048 < N <= 4096: split in-LDS build
     ([300, 100000, 3, 5_000_000], 64, 6000, 1.1, torch.float32),       # N > 4096: split hash build
     ([5, 100000, 3, 77] * 6 + [9, 10], 128, 8192, None, torch.bfloat16),  # configs[2] shape (bf16, B=8192)
     ([50] * 40, 32, 200, None, torch.float32),                         # F = 41: unsplit fallback
+    ([50] * 40, 32, 6000, None, torch.float32),                        # F = 41, N > 4096: unsplit hash build
     ([1], 16, 64, None, torch.float32),                                # every position hits one row
     ([10, 3000, 7, 100000, 3], 256, 512, 1.2, torch.float32)])         # 1-KB rows: 4 chunks per lane group
 def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
