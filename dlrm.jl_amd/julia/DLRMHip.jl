@@ -286,4 +286,62 @@ function EmbeddingTables.update!(
     return nothing
 end
 
+#####
+##### Optional fast path: the sparse half of one train! iteration as the training-step pair
+##### (dlrm_step_fwd / dlrm_step_bwd): identical results to maplookup -> interaction ->
+##### dot_back -> update!, three launches instead of five.
+#####
+
+"""
+    HipTrainStep(ctx, tables, batch; lr)
+
+Buffers of one training step (out, dx, dt) and the step's indexer.  `train_step_fwd!` returns
+the interaction output for the top MLP; `train_step_bwd!` takes dLoss/d(out) and returns dx,
+updating the tables in place (rows hit once by the backward, the rest by the apply).
+"""
+mutable struct HipTrainStep{T}
+    ctx::Context
+    tables::Vector{HipEmbedding}
+    ix::HipIndexer
+    out::DeviceMatrix{T}
+    dx::DeviceMatrix{Float32}
+    dt::DeviceMatrix{Float32}
+    idx::Union{Nothing,PackedIndices}
+    x::Union{Nothing,DeviceMatrix{T}}
+    padding::Int
+    lr::Float32
+end
+function HipTrainStep(ctx::Context, tables::AbstractVector{<:HipEmbedding{Static{D},T}}, batch::Integer;
+                      lr = 0.01, pad_to = 1) where {D,T}
+    F = length(tables) + 1
+    width, padding = interaction_sizes(D, F, pad_to)
+    return HipTrainStep{T}(ctx, collect(tables), HipIndexer(ctx, length(tables), batch),
+                           DeviceMatrix{T}(ctx, width, batch), DeviceMatrix{Float32}(ctx, D, batch),
+                           DeviceMatrix{Float32}(ctx, F * D, batch), nothing, nothing, padding, Float32(lr))
+end
+
+function train_step_fwd!(st::HipTrainStep{T}, x::AbstractMatrix{T}, sparse) where {T}
+    d, B = size(x)
+    st.idx = sparse isa PackedIndices ? sparse : pack(st.ctx, sparse)
+    st.x = x isa DeviceMatrix ? x : upload!(DeviceMatrix{T}(st.ctx, d, B), x)
+    check(st.ctx, ccall((:dlrm_step_fwd, libdlrm), Cint,
+                        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
+                         Ptr{Cvoid}, Int64, Cint),
+                        st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
+                        st.x.ptr, d, st.out.ptr, size(st.out, 1), st.padding))
+    return Array(st.out)
+end
+
+function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}) where {T}
+    d, B = size(st.x)
+    Δd = upload!(DeviceMatrix{T}(st.ctx, size(Δ)...), Matrix{T}(Δ))
+    check(st.ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
+                        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
+                         Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat, Cuint),
+                        st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
+                        st.x.ptr, d, Δd.ptr, size(Δ, 1), st.padding, st.dx.ptr, d, st.dt.ptr, size(st.dt, 1),
+                        st.lr, Cuint(0)))
+    return Array(st.dx)
+end
+
 end # module

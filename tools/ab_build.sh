@@ -9,7 +9,7 @@ for f in abi.cpp lookup.hip interact.hip update.hip common.hpp indexer.hpp; do
 done
 git show "$REV:include/dlrm_hip.h" > "$DIR/r/include/dlrm_hip.h"
 cd "$DIR/r/pkg/csrc"
-for f in abi.cpp lookup.hip interact.hip update.hip; do
+for f in abi.cpp lookup.hip interact.hip update.hip hashindex.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=fast -x hip -c $f -o $f.o &
 done
 wait

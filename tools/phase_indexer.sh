@@ -5,7 +5,7 @@ set -e
 BLK=${1:-2}
 D=dlrm.jl_amd/csrc
 mkdir -p /tmp/dlrm_phase
-for f in abi.cpp lookup.hip interact.hip update.hip; do
+for f in abi.cpp lookup.hip interact.hip update.hip hashindex.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=fast -DDLRM_PHASE=$BLK -x hip -c $D/$f -o /tmp/dlrm_phase/$f.o &
 done
 wait

@@ -4,7 +4,7 @@
 set -e
 D=dlrm.jl_amd/csrc
 mkdir -p /tmp/dlrm_wt
-for f in abi.cpp lookup.hip interact.hip update.hip; do
+for f in abi.cpp lookup.hip interact.hip update.hip hashindex.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=fast -DDLRM_WTRACE -x hip -c $D/$f -o /tmp/dlrm_wt/$f.o &
 done
 wait
