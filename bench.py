@@ -240,8 +240,13 @@ def main():
             for k in range(max(a.warmup, 1)):
                 step(k)
             torch.cuda.synchronize()
-            prepare_graphs()
-            a.mode = "segments"
+            try:
+                prepare_graphs()
+                a.mode = "segments"
+            except Exception as e:  # capture refused: eager launches (same work)
+                print(f"note: segment graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
+                engine._graphs = None
+                a.mode = "eager"
 
     # warm-up (also validates indices once)
     for k in range(max(a.warmup, 1)):
