@@ -26,6 +26,16 @@
 #include <cstdlib>
 
 #include "common.hpp"
+
+#ifdef DLRM_PHASE
+// Phase timestamps of the split indexer inside the step forward's launch (table DLRM_PHASE);
+// only in the profiling variant of the library (tools/phase_stepfwd.py).
+__device__ unsigned long long g_phase_fwd[64];
+#define PHASE(k) do { __syncthreads(); if (blockIdx.x == DLRM_PHASE && threadIdx.x == 0) g_phase_fwd[k] = wall_clock64(); } while (0)
+extern "C" int dlrm_debug_phase_fwd(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_fwd), sizeof(g_phase_fwd));
+}
+#endif
 #include "indexer.hpp"
 
 #ifdef DLRM_WTRACE
