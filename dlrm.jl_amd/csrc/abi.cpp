@@ -7,6 +7,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -38,6 +39,7 @@ struct dlrm_tables {
 struct dlrm_indexer {
     dlrm_ctx* ctx = nullptr;
     int T = 0;
+    int TV = 0;  // tables of the per-table arrays: 4T when the forward launch may split tables by row bits
     IndexerDev dev{};
     void* block = nullptr;  // one allocation for every array
     void* partial_big = nullptr;  // partial rows for D > kPartialDim (allocated on first use)
@@ -364,6 +366,7 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer*
                   "dlrm_interact_bwd_gather: batch*lookups %lld > indexer capacity %lld", (long long)batch * lookups,
                   (long long)ix->dev.cap);
     }
+    if (ix) ix->dev.vshift = 0;
     rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                     index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld,
                                     ix ? &ix->dev : nullptr);
@@ -384,7 +387,13 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->ctx = ctx;
     ix->T = num_tables;
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
-    const int64_t T = num_tables > 0 ? num_tables : 1;
+    const int64_t T0 = num_tables > 0 ? num_tables : 1;
+    // the forward launch's indexer (batch <= kStepIndexMaxN) sorts each table as up to
+    // kStepMaxParts parts (by the low bits of the row): the per-table arrays then hold that many
+    // virtual tables per table (the hash arrays, single[] and the global sort scratch stay per
+    // real table)
+    const int64_t T = cap <= kStepIndexMaxN ? kStepMaxParts * T0 : T0;
+    ix->TV = (int)T;
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
     ix->dev.pdim = kPartialDim;
@@ -394,18 +403,18 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     while (((int64_t)1 << ix->dev.hbits) < hs) ++ix->dev.hbits;
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
-    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1));
+    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1)), n0 = (size_t)(T0 * cap);
     Piece pieces[] = {
-        {(void**)&ix->dev.keys0, n * 4},     {(void**)&ix->dev.keys1, n * 4},   {(void**)&ix->dev.vals0, n * 4},
-        {(void**)&ix->dev.vals1, n * 4},     {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
+        {(void**)&ix->dev.keys0, n0 * 4},    {(void**)&ix->dev.keys1, n0 * 4},  {(void**)&ix->dev.vals0, n0 * 4},
+        {(void**)&ix->dev.vals1, n0 * 4},    {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
         {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot, n * 16},
         {(void**)&ix->dev.hot_slice, n * 4}, {(void**)&ix->dev.hot_cnt, n * 4},
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
-        {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n},
+        {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
-        {(void**)&ix->dev.pslot, hs ? n * 4 : 0},    {(void**)&ix->dev.hent, (size_t)(T * hs) * 8},
-        {(void**)&ix->dev.hseg, (size_t)(T * hs) * 8},
-        {(void**)&ix->dev.hfill, (size_t)(T * hs) * 4}, {(void**)&ix->dev.hstate, hs ? (size_t)T * 32 : 0},
+        {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
+        {(void**)&ix->dev.hseg, (size_t)(T0 * hs) * 8},
+        {(void**)&ix->dev.hfill, (size_t)(T0 * hs) * 4}, {(void**)&ix->dev.hstate, hs ? (size_t)T0 * 32 : 0},
     };
     size_t total = 0;
     for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
@@ -423,7 +432,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         base += (pc.bytes + 255) & ~(size_t)255;
     }
     if (hs) {  // every slot starts empty (the alloc pass resets the slots it used)
-        rc = ctx_hip(ctx, hipMemset(ix->dev.hent, 0xff, (size_t)(T * hs) * 8), "hipMemset(hash slots)");
+        rc = ctx_hip(ctx, hipMemset(ix->dev.hent, 0xff, (size_t)(T0 * hs) * 8), "hipMemset(hash slots)");
         if (rc != DLRM_OK) {
             (void)hipFree(ix->block);
             delete ix;
@@ -450,6 +459,7 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_build: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG((int64_t)batch * lookups <= ix->dev.cap, "dlrm_indexer_build: batch*lookups %lld > capacity %lld",
               (long long)batch * lookups, (long long)ix->dev.cap);
+    ix->dev.vshift = 0;
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups);
     if (rc) return rc;
     record_build(ix, false, indices, itype, table_stride, index_base, batch, lookups);
@@ -465,11 +475,35 @@ int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables*
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_build_split: batch %d > capacity %lld", batch,
               (long long)ix->dev.cap);
     ix->built = false;
+    ix->dev.vshift = 0;
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, 1,
                               true, nullptr);
     if (rc) return rc;
     record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
     return DLRM_OK;
+}
+
+// One (virtual) table's build, whole: rows, grouped positions, segment starts.
+struct IndexerTable {
+    std::vector<uint32_t> rows;
+    std::vector<int32_t> perm, seg_start;
+};
+static int read_indexer_table(dlrm_ctx* ctx, const dlrm_indexer* ix, int v, IndexerTable& o) {
+    int32_t cnt[8];
+    int rc = ctx_hip(ctx, hipMemcpy(cnt, ix->dev.counts + (int64_t)v * 8, sizeof(cnt), hipMemcpyDeviceToHost), "read");
+    if (rc) return rc;
+    const int64_t U = cnt[0], NV = cnt[4];
+    const int64_t off = (int64_t)v * ix->dev.cap;
+    o.rows.resize(U);
+    o.perm.resize(NV);
+    o.seg_start.resize(U + 1);
+    if (U) rc = ctx_hip(ctx, hipMemcpy(o.rows.data(), ix->dev.seg_row + off, U * 4, hipMemcpyDeviceToHost), "read");
+    if (rc == DLRM_OK && NV)
+        rc = ctx_hip(ctx, hipMemcpy(o.perm.data(), ix->dev.perm + off, NV * 4, hipMemcpyDeviceToHost), "read");
+    if (rc == DLRM_OK)
+        rc = ctx_hip(ctx, hipMemcpy(o.seg_start.data(), ix->dev.seg_start + (int64_t)v * (ix->dev.cap + 1),
+                                    (U + 1) * 4, hipMemcpyDeviceToHost), "read");
+    return rc;
 }
 
 int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t* num_unique, int64_t* rows,
@@ -479,31 +513,37 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t*
     CHECK_ARG(table >= 0 && table < ix->T, "dlrm_indexer_read: table %d", table);
     int rc = ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     if (rc) return rc;
-    int32_t cnt[8];
-    rc = ctx_hip(ctx, hipMemcpy(cnt, ix->dev.counts + (int64_t)table * 8, sizeof(cnt), hipMemcpyDeviceToHost), "read");
+    IndexerTable tt;
+    if (ix->dev.vshift == 0) {
+        rc = read_indexer_table(ctx, ix, table, tt);
+    } else {
+        // a forward-launch build: merge the table's parts (each sorted by row)
+        const int np = 1 << ix->dev.vshift;
+        IndexerTable h[kStepMaxParts];
+        for (int q = 0; q < np && rc == DLRM_OK; ++q) rc = read_indexer_table(ctx, ix, table * np + q, h[q]);
+        size_t k[kStepMaxParts] = {};
+        tt.seg_start.assign(1, 0);
+        for (;;) {
+            int e = -1;
+            for (int q = 0; q < np && rc == DLRM_OK; ++q)
+                if (k[q] < h[q].rows.size() && (e < 0 || h[q].rows[k[q]] < h[e].rows[k[e]])) e = q;
+            if (e < 0) break;
+            const size_t u = k[e]++;
+            tt.rows.push_back(h[e].rows[u]);
+            for (int32_t i = h[e].seg_start[u]; i < h[e].seg_start[u + 1]; ++i) tt.perm.push_back(h[e].perm[i]);
+            tt.seg_start.push_back((int32_t)tt.perm.size());
+        }
+    }
     if (rc) return rc;
-    *num_unique = cnt[0];
-    const int64_t U = cnt[0], NV = cnt[4];
-    const int64_t off = (int64_t)table * ix->dev.cap;
-    if (rows) {
-        const int64_t n = U < cap ? U : cap;
-        std::vector<uint32_t> tmp(n > 0 ? n : 1);
-        if (n) rc = ctx_hip(ctx, hipMemcpy(tmp.data(), ix->dev.seg_row + off, n * 4, hipMemcpyDeviceToHost), "read");
-        for (int64_t i = 0; i < n; ++i) rows[i] = tmp[i];
+    const int64_t U = (int64_t)tt.rows.size(), NV = (int64_t)tt.perm.size();
+    *num_unique = U;
+    if (rows)
+        for (int64_t i = 0; i < U && i < cap; ++i) rows[i] = tt.rows[i];
+    if (positions && seg_start) {
+        for (int64_t i = 0; i < NV && i < cap; ++i) positions[i] = tt.perm[i];
+        for (int64_t i = 0; i <= U && i <= cap; ++i) seg_start[i] = tt.seg_start[i];
     }
-    if (positions && seg_start && rc == DLRM_OK) {
-        const int64_t n = NV < cap ? NV : cap;
-        std::vector<int32_t> tmp((n > 0 ? n : 1));
-        if (n) rc = ctx_hip(ctx, hipMemcpy(tmp.data(), ix->dev.perm + off, n * 4, hipMemcpyDeviceToHost), "read");
-        for (int64_t i = 0; i < n; ++i) positions[i] = tmp[i];
-        const int64_t ns = (U + 1) < (cap + 1) ? (U + 1) : (cap + 1);
-        std::vector<int32_t> tmp2(ns);
-        if (rc == DLRM_OK)
-            rc = ctx_hip(ctx, hipMemcpy(tmp2.data(), ix->dev.seg_start + (int64_t)table * (ix->dev.cap + 1), ns * 4,
-                                        hipMemcpyDeviceToHost), "read");
-        for (int64_t i = 0; i < ns; ++i) seg_start[i] = tmp2[i];
-    }
-    return rc;
+    return DLRM_OK;
 }
 
 // multi-slice hot segments keep partial rows of D elements (allocated on first use for D > kPartialDim;
@@ -513,7 +553,7 @@ static int ensure_partials(dlrm_ctx* ctx, dlrm_indexer* ix, int D) {
     void* p = nullptr;
     int rc = hip_set(ctx);
     if (rc == DLRM_OK)
-        rc = ctx_hip(ctx, hipMalloc(&p, (size_t)(ix->T > 0 ? ix->T : 1) * (size_t)ix->dev.pcap * D * 4),
+        rc = ctx_hip(ctx, hipMalloc(&p, (size_t)ix->TV * (size_t)ix->dev.pcap * D * 4),
                      "hipMalloc(indexer partials)");
     if (rc) return rc;
     if (ix->partial_big) (void)hipFree(ix->partial_big);
@@ -570,6 +610,14 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     CHECK_ARG(padding >= 0 && x_ld >= d && out_ld >= d + P + padding, "dlrm_step_fwd: leading dimensions too small");
     CHECK_ARG(batch == 0 || (x && out), "dlrm_step_fwd: null buffer");
     ix->built = false;
+    // parts per table in the forward launch's indexer (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides, for
+    // comparison)
+    static const int parts_log2 = [] {
+        const char* e = getenv("DLRM_STEP_PARTS");
+        const int p = e ? atoi(e) : kStepParts;
+        return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
+    }();
+    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? parts_log2 : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev);
     if (rc == DLRM_OK) {
@@ -577,6 +625,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         return DLRM_OK;
     }
     if (rc != DLRM_E_UNSUPPORTED) return rc;
+    ix->dev.vshift = 0;
     const bool split_ok = step_split_supported(tb->aligned16, tb->T, tb->dtype, d, x, x_ld);
     if (split_ok && batch <= kFastMaxN) {
         // no single-launch form for this shape (B > 2048): the fused forward, then the split

@@ -154,6 +154,12 @@ struct OutMap {
 
 constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions per table
 constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
+constexpr int kStepIndexMaxN = 2048;  // the forward-launch indexer (interact.hip): positions per table
+constexpr int kStepMaxParts = 8;      // ... which sorts a table as up to 8 parts (by the row's low bits)
+#ifndef DLRM_STEP_PARTS_DEFAULT
+#define DLRM_STEP_PARTS_DEFAULT 4
+#endif
+constexpr int kStepParts = DLRM_STEP_PARTS_DEFAULT;
 
 struct IndexerDev {
     uint32_t* keys0;  uint32_t* keys1;   // global sort scratch (cap > kLdsSortMax)
@@ -175,6 +181,11 @@ struct IndexerDev {
     uint32_t* hfill;       // [T][hsize] placement cursor
     unsigned long long* hstate;  // [T][4] {segments << 32 | positions} allocation cursor, ...
     int64_t hsize;         // slots per table (power of two >= 2 cap), 0 = no hash arrays
+    // > 0: the build split each table's positions by the row's low vshift bits into virtual
+    // tables v = (t << vshift) + (row & mask) (the forward launch's indexer: 2^vshift workgroups
+    // per table); the per-table arrays above (perm ... counts, not single / pslot / hash) are then
+    // indexed by v, and the apply maps v -> t.
+    int vshift;
     int hbits;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)

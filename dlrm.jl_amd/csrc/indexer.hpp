@@ -63,10 +63,10 @@ __device__ __forceinline__ V block_scan_nw(V v, V* wtot, V* tot) {
 // NT threads (1024 standalone; 256 inside the backward launch), EPL positions per thread.
 // Digit width: 8 bits with 16 waves, 11 bits with 4 (about one key per bucket at N = 2048, so
 // the within-bucket rank is short where one wave per SIMD hides no latency).
-template <int NT, int EPL>
+template <int NT, int EPL, int DB_ = (NT >= 1024 ? 8 : 11)>
 struct FastLds {
     static constexpr int NW = NT / 64;
-    static constexpr int DB = NT >= 1024 ? 8 : 11;  // digit bits
+    static constexpr int DB = DB_;                  // digit bits
     static constexpr int ND = 1 << DB;              // digits
     static constexpr int CPT = ND * NW / NT;        // (digit, wave) counters per thread: 4 or 32
     static_assert(CPT == 4 || CPT % 8 == 0, "counters per thread: 4, or whole uint4s");
@@ -80,17 +80,17 @@ struct FastLds {
 };
 
 // One stable counting pass.  FROM_REGS: the first pass's keys come from registers (tile j
-// of wave w = position w*S + 64j + lane); otherwise from kin/vin[0, n) in LDS.  Returns the
+// of wave w = position w*S + 64j + lane, S = 64*EPL); otherwise from kin/vin[0, n) in LDS,
+// wave w taking [w*S, (w+1)*S) for the caller's S (a multiple of 64, S*NW >= n).  Returns the
 // number of keys written to kout/vout.
-template <int NT, int EPL, bool FROM_REGS>
+template <int NT, int EPL, bool FROM_REGS, int DB>
 __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bool (&rok)[EPL],
                          const uint32_t* kin, const int32_t* vin, uint32_t* kout, int32_t* vout,
-                         FastLds<NT, EPL>& sl, bool first) {
-    typedef FastLds<NT, EPL> FL;
+                         FastLds<NT, EPL, DB>& sl, bool first, int S = 64 * EPL) {
+    typedef FastLds<NT, EPL, DB> FL;
     constexpr int CPT = FL::CPT, NW = FL::NW;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    constexpr int S = 64 * EPL;
     if (CPT == 4) {
         ((uint2*)&sl.cnt[0][0])[tid] = make_uint2(0, 0);
     } else {
@@ -109,7 +109,7 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
             ok[j] = rok[j];
             val[j] = i;
         } else {
-            ok[j] = i < n;
+            ok[j] = j * 64 < S && i < n;
             key[j] = ok[j] ? kin[i] : 0u;
             val[j] = ok[j] ? vin[i] : 0;
         }
@@ -117,6 +117,7 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
+        if (j * 64 >= S) break;  // uniform
         const uint32_t d = (key[j] >> shift) & (FL::ND - 1);
         unsigned long long peers = __ballot(ok[j]);
 #pragma unroll
@@ -198,13 +199,19 @@ __device__ int fast_pass(int n, int shift, const uint32_t (&rkey)[EPL], const bo
 
 // SPLIT (the training step's build, run before a backward that updates once-hit rows itself):
 // segments of one position get no chunk, and single[p] = 1 marks each such position p.
-template <int NT, int EPL, bool SPLIT = false>
-__device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, const void* __restrict__ idx,
-                                 int itype, int64_t tstride, int base, int N, unsigned* __restrict__ err,
-                                 FastLds<NT, EPL>& sl) {
+// vs = 0: every position of table t, results under index v = t.  vs = 1 / 2: only the
+// positions whose row has low bits == v mod 2^vs (virtual table v = (t << vs) + part,
+// IndexerDev::vshift = vs): they are compacted in position order, sorted on row >> vs, and
+// the rows written back whole.  2^vs workgroups then share a table's positions.
+template <int NT, int EPL, bool SPLIT = false, int DB>
+__device__ void fast_index_table(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows,
+                                 const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
+                                 unsigned* __restrict__ err, FastLds<NT, EPL, DB>& sl) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int S = 64 * EPL;
-    const int nbits = 32 - __clz(nrows > 0 ? nrows - 1 : 0);
+    const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
+    const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
+    const int nbits = 32 - __clz(kmax);
     // the indices, read once (coalesced 64-lane runs, all loads in flight) and validated
     uint32_t key[EPL];
     bool ok[EPL];
@@ -220,13 +227,46 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
         const int64_t r = raw[j] - base;
         ok[j] = i < N && r >= 0 && r < (int64_t)nrows;
         key[j] = ok[j] ? (uint32_t)r : 0u;
-        if (i < N && !ok[j]) raise_index_error(err);
+        if (i < N && !ok[j] && part == 0) raise_index_error(err);
     }
     PHASE(1);
-    const int n = fast_pass<NT, EPL, true>(N, 0, key, ok, nullptr, nullptr, sl.K[1], sl.V[1], sl, true);
+    int n, SW = S;  // keys; positions per wave in the counting passes
+    if (vs == 0) {
+        n = fast_pass<NT, EPL, true>(N, 0, key, ok, nullptr, nullptr, sl.K[1], sl.V[1], sl, true);
+    } else {
+        // stable compaction of this half's positions (position order = wave, tile, lane order)
+        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        int run = 0, lr[EPL];
+        bool keep[EPL];
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) {
+            keep[j] = ok[j] && (key[j] & ((1u << vs) - 1u)) == part;
+            const unsigned long long b = __ballot(keep[j]);
+            lr[j] = run + __popcll(b & lt);
+            run += __popcll(b);
+        }
+        if (lane == 0) sl.wtot[w] = run;
+        __syncthreads();
+        int wb = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < NT / 64; ++k) {
+            const int c = sl.wtot[k];
+            wb += k < w ? c : 0;
+            tot += c;
+        }
+#pragma unroll
+        for (int j = 0; j < EPL; ++j)
+            if (keep[j]) {
+                sl.K[0][wb + lr[j]] = key[j] >> vs;
+                sl.V[0][wb + lr[j]] = w * S + j * 64 + lane;
+            }
+        __syncthreads();
+        SW = 64 * ((tot + NT - 1) / NT);
+        n = fast_pass<NT, EPL, false>(tot, 0, key, ok, sl.K[0], sl.V[0], sl.K[1], sl.V[1], sl, true, SW);
+    }
     PHASE(5);
     int cur = 1;
-    typedef FastLds<NT, EPL> FL;
+    typedef FastLds<NT, EPL, DB> FL;
     if (nbits > FL::DB) {
         if (sl.maxbucket <= kRankBucketMax) {
             // order each bucket by (row, position); the stable pass kept positions ascending
@@ -239,7 +279,7 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
 #pragma unroll
                 for (int q = 0; q < EPL; ++q) {
                     const int i = tid + q * NT;
-                    ki[q] = i < n ? sl.K[1][i] : 0u;
+                    ki[q] = (q * NT < n && i < n) ? sl.K[1][i] : 0u;
                 }
 #pragma unroll
                 for (int q = 0; q < EPL; ++q) {
@@ -253,7 +293,7 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
                 for (int j = 0; j < maxlen; ++j) {
 #pragma unroll
                     for (int q = 0; q < EPL; ++q)
-                        if (j < len[q]) {
+                        if (q * NT < n && j < len[q]) {
                             const uint32_t kj = sl.K[1][bs[q] + j];
                             rank[q] += (kj < ki[q] || (kj == ki[q] && bs[q] + j < (int)(tid + q * NT))) ? 1 : 0;
                         }
@@ -293,20 +333,22 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
             cur = 0;
         } else {
             for (int shift = FL::DB; shift < nbits; shift += FL::DB) {
-                fast_pass<NT, EPL, false>(n, shift, key, ok, sl.K[cur], sl.V[cur], sl.K[cur ^ 1], sl.V[cur ^ 1], sl, false);
+                fast_pass<NT, EPL, false>(n, shift, key, ok, sl.K[cur], sl.V[cur], sl.K[cur ^ 1], sl.V[cur ^ 1], sl,
+                                          false, SW);
                 cur ^= 1;
             }
         }
     }
     PHASE(10);
-    // ---- segments: thread tid owns sorted entries [EPL*tid, EPL*tid + EPL)
+    // ---- segments: thread tid owns sorted entries [E*tid, E*tid + E)
+    const int E = (n + NT - 1) / NT;  // <= EPL
     const uint32_t* K = sl.K[cur];
     const int32_t* Vs = sl.V[cur];
     int32_t* sseg = sl.V[cur ^ 1];
     uint32_t* srow = sl.K[cur ^ 1];
-    const int64_t off = (int64_t)t * ix.cap;
+    const int64_t off = (int64_t)v * ix.cap;
     int32_t* perm = ix.perm + off;
-    int32_t* seg_start = ix.seg_start + (int64_t)t * (ix.cap + 1);
+    int32_t* seg_start = ix.seg_start + (int64_t)v * (ix.cap + 1);
     uint32_t* seg_row = ix.seg_row + off;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
@@ -318,10 +360,11 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
     uint32_t kq[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
-        const int i = EPL * tid + q;
-        kq[q] = i < n ? K[i] : 0u;
-        const uint32_t kp = (i > 0 && i < n) ? K[i - 1] : ~kq[q];
-        head[q] = i < n && kp != kq[q];
+        const int i = E * tid + q;
+        const bool in = q < E && i < n;
+        kq[q] = in ? K[i] : 0u;
+        const uint32_t kp = (in && i > 0) ? K[i - 1] : ~kq[q];
+        head[q] = in && kp != kq[q];
         h += head[q] ? 1 : 0;
     }
     int U;
@@ -329,20 +372,21 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
 #pragma unroll
     for (int q = 0; q < EPL; ++q)
         if (head[q]) {
-            const int i = EPL * tid + q;
+            const int i = E * tid + q;
+            const uint32_t row = (kq[q] << vs) | part;
             sseg[s] = i;
-            srow[s] = kq[q];
+            srow[s] = row;
             seg_start[s] = i;
-            seg_row[s] = kq[q];
+            seg_row[s] = row;
             ++s;
         }
     if (tid == 0) seg_start[U] = n;
     if (SPLIT) {  // once-hit positions: head of a segment whose next entry starts another
-        uint8_t* single = ix.single + off;
+        uint8_t* single = ix.single + (int64_t)t * ix.cap;
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
-            const int i = EPL * tid + q;
-            if (i < n) single[Vs[i]] = (head[q] && (i + 1 == n || K[i + 1] != kq[q])) ? 1 : 0;
+            const int i = E * tid + q;
+            if (q < E && i < n) single[Vs[i]] = (head[q] && (i + 1 == n || K[i + 1] != kq[q])) ? 1 : 0;
         }
     }
     __syncthreads();
@@ -353,9 +397,9 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
     int beg[EPL], end[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
-        const int sidx = EPL * tid + q;
+        const int sidx = E * tid + q;
         beg[q] = end[q] = 0;
-        if (sidx < U) {
+        if (q < E && sidx < U) {
             beg[q] = sseg[sidx];
             end[q] = sidx + 1 < U ? sseg[sidx + 1] : n;
             const int len = end[q] - beg[q];
@@ -371,8 +415,8 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
     int32_t* hot_slice = ix.hot_slice + off;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
-        const int sidx = EPL * tid + q;
-        if (sidx < U) {
+        const int sidx = E * tid + q;
+        if (q < E && sidx < U) {
             const int len = end[q] - beg[q];
             if (SPLIT && len == 1) {
                 // updated by the backward (single[] flag)
@@ -388,7 +432,7 @@ __device__ void fast_index_table(const IndexerDev& ix, int t, uint32_t nrows, co
         }
     }
     if (tid == 0) {
-        int32_t* cnt = ix.counts + (int64_t)t * 8;
+        int32_t* cnt = ix.counts + (int64_t)v * 8;
         cnt[CNT_U] = U; cnt[CNT_C] = (int)(tot64 & M21); cnt[CNT_H] = (int)((tot64 >> 21) & M21);
         cnt[CNT_S] = (int)((tot64 >> 42) & M21); cnt[CNT_NV] = n;
     }
@@ -423,22 +467,38 @@ __device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb,
     }
 }
 
-// Per-wave prefix of one count over the tables (T <= 64 kept in registers; more tables are
-// re-scanned tile by tile on every lookup).
+// Per-wave prefix of one count over the tables.  T <= 64 * kScanTiles: lane l holds the counts
+// of the G = ceil(T / 64) consecutive tables [l*G, l*G + G) and the inclusive prefix of their
+// sums, so a lookup is one binary lifting over the lanes plus G independent shuffles.  More
+// tables are re-scanned tile by tile on every lookup.
+constexpr int kScanTiles = 4;
 struct TableScan {
-    int incl;   // this lane's inclusive prefix (tile 0)
-    int total;  // over all tables
+    int cnt[kScanTiles];  // counts of this lane's tables
+    int incl;             // inclusive prefix over the lanes' groups
+    int total;            // over all tables
+    int G;                // tables per lane (0: T > 64 * kScanTiles)
 };
 
 __device__ __forceinline__ TableScan scan_counts(const IndexerDev& ix, int T_, int which) {
     const int lane = threadIdx.x & 63;
-    TableScan r{0, 0};
+    TableScan r{};
+    if (T_ <= 64 * kScanTiles) {
+        r.G = (T_ + 63) / 64;
+        int sum = 0;
+#pragma unroll
+        for (int q = 0; q < kScanTiles; ++q) {  // every load in flight
+            const int v = lane * r.G + q;
+            r.cnt[q] = (q < r.G && v < T_) ? ix.counts[(int64_t)v * 8 + which] : 0;
+            sum += r.cnt[q];
+        }
+        r.incl = wave_incl_scan(sum);
+        r.total = __shfl(r.incl, 63, 64);
+        return r;
+    }
     for (int tb = 0; tb < T_; tb += 64) {
         const int tt = tb + lane;
         const int c = tt < T_ ? ix.counts[(int64_t)tt * 8 + which] : 0;
-        const int incl = wave_incl_scan(c);
-        if (tb == 0) r.incl = incl;
-        r.total += __shfl(incl, 63, 64);
+        r.total += __shfl(wave_incl_scan(c), 63, 64);
     }
     return r;
 }
@@ -447,8 +507,24 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
                                        int& table, int& local) {
     table = -1;
     local = 0;
-    if (T_ <= 64) {
+    if (sc.G == 1) {
         locate_in_tile(sc.incl, sc.total, 0, id, table, local);
+        return;
+    }
+    if (sc.G > 1) {
+        int grp = -1, loc = 0;
+        locate_in_tile(sc.incl, sc.total, 0, id, grp, loc);
+        const int src = grp < 0 ? 0 : grp;
+        int run = 0;
+#pragma unroll
+        for (int q = 0; q < kScanTiles; ++q) {
+            const int c = __shfl(sc.cnt[q], src, 64);
+            if (grp >= 0 && table < 0 && q < sc.G && loc < run + c) {
+                table = src * sc.G + q;
+                local = loc - run;
+            }
+            run += c;
+        }
         return;
     }
     const int lane = threadIdx.x & 63;

@@ -273,24 +273,33 @@ __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F,
 }
 
 // The forward of a training step with the SparseIndexer build in the same grid (split form:
-// once-hit positions flagged for the backward, the rest listed for the apply): workgroups
-// [0, T) each sort one table's positions (indexer.hpp, 256 threads), the rest run the fused
-// lookup + interaction without ys.  The indexer depends only on the indices, so it streams
-// beside the gather instead of adding a launch.
-constexpr int kStepIndexEPL = 8;  // positions per thread: N <= 2048
+// once-hit positions flagged for the backward, the rest listed for the apply): the first
+// T << ix.vshift workgroups sort the tables' positions (indexer.hpp, 256 threads; with
+// vshift = 1 two per table, one per row parity, which halves the critical path), the rest run
+// the fused lookup + interaction without ys.  The indexer depends only on the indices, so it
+// streams beside the gather instead of adding a launch.
+constexpr int kStepIndexEPL = kStepIndexMaxN / 256;  // positions per thread
+#ifndef DLRM_STEP_DB
+#define DLRM_STEP_DB 8
+#endif
+// 8-bit digits: a table part holds about N >> vshift positions, and the digit scan (NW << DB
+// counters) is a fixed cost of every counting pass
+typedef FastLds<256, kStepIndexEPL, DLRM_STEP_DB> StepLds;
 template <typename T, int NB, int DC = 0>
 __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                  int64_t x_ld, T* __restrict__ out, int64_t out_ld,
                                                                  int padding, GatherArgs ga, IndexerDev ix) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int T_ = F - 1;
-    if ((int)blockIdx.x < T_) {
-        FastLds<256, kStepIndexEPL>& sl = *(FastLds<256, kStepIndexEPL>*)smem;
-        fast_index_table<256, kStepIndexEPL, true>(ix, blockIdx.x, (uint32_t)ga.tabs[blockIdx.x].nrows, ga.idx,
-                                                   ga.itype, ga.tstride, ga.base, B * ga.L, ga.err, sl);
+    const int NI = T_ << ix.vshift;
+    if ((int)blockIdx.x < NI) {
+        StepLds& sl = *(StepLds*)smem;
+        const int v = blockIdx.x, t = v >> ix.vshift;
+        fast_index_table<256, kStepIndexEPL, true>(ix, v, t, ix.vshift, (uint32_t)ga.tabs[t].nrows, ga.idx, ga.itype,
+                                                   ga.tstride, ga.base, B * ga.L, ga.err, sl);
         return;
     }
-    fwd_body<T, NB, true, 4, false, DC>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, x, x_ld, nullptr, 0, out,
+    fwd_body<T, NB, true, 4, false, DC>(blockIdx.x - NI, gridDim.x - NI, smem, d, F, B, x, x_ld, nullptr, 0, out,
                                         out_ld, padding, ga);
 }
 
@@ -552,8 +561,8 @@ __global__ __launch_bounds__(256, 3) void interact_bwd_index_kernel(int d, int F
     const int T_ = F - 1;
     if ((int)blockIdx.x < T_) {
         FastLds<256, kBwdIndexEPL>& sl = *(FastLds<256, kBwdIndexEPL>*)smem;
-        fast_index_table<256, kBwdIndexEPL>(ix, blockIdx.x, (uint32_t)ga.tabs[blockIdx.x].nrows, ga.idx, ga.itype,
-                                            ga.tstride, ga.base, B * ga.L, ga.err, sl);
+        fast_index_table<256, kBwdIndexEPL>(ix, blockIdx.x, blockIdx.x, 0, (uint32_t)ga.tabs[blockIdx.x].nrows,
+                                            ga.idx, ga.itype, ga.tstride, ga.base, B * ga.L, ga.err, sl);
         return;
     }
     bwd_body<T, NB, true, false, 1>(blockIdx.x - T_, gridDim.x - T_, smem, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt,
@@ -852,14 +861,14 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
     if (B == 0 || T_ == 0 || !tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, nullptr, 0) || NB > 2 ||
-        B > 256 * kStepIndexEPL)
+        B > kStepIndexMaxN)
         return DLRM_E_UNSUPPORTED;
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
-    size_t lds = sizeof(FastLds<256, kStepIndexEPL>);
+    size_t lds = sizeof(StepLds);
     if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
-    const unsigned g = grid_for(B, 4, cus) + T_;
+    const unsigned g = grid_for(B, 4, cus) + (T_ << ix.vshift);
 #define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
     if (d == 128)                                                                                                  \
         hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_, 128>), dim3(g), dim3(256), lds, s, d, F, B,            \

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
     if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
 #endif
     PHASE(0);
-    fast_index_table<NT, EPL, SPLIT>(ix, t, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
+    fast_index_table<NT, EPL, SPLIT>(ix, t, t, 0, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
 #endif
@@ -476,9 +476,9 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
             locate(ix, T_, CNT_C, sC, (item - sS.total) * NG + gid, tc, cl);
             if (g >= G::RPW || tc < 0) continue;
             const int64_t off = (int64_t)tc * ix.cap;
-            const GT* gbase = grad + grad_offset + (int64_t)tc * D;
+            const GT* gbase = grad + grad_offset + (int64_t)(tc >> ix.vshift) * D;
             const int4 cd = ix.chunks[off + cl];
-            TT* row = (TT*)tabs[tc].data + (int64_t)(uint32_t)cd.z * D;
+            TT* row = (TT*)tabs[tc >> ix.vshift].data + (int64_t)(uint32_t)cd.z * D;
             float tv[G::VPL][NE];
 #pragma unroll
             for (int j = 0; j < G::VPL; ++j) load_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
             int32_t* stage = hot_stage[gid];
             for (int k = v; k < m; k += G::LPR) stage[k] = perm[b0 + k];
             wave_lds_sync();
-            sum_staged<GT, VPR>(stage, m, L, grad + grad_offset + (int64_t)th * D, grad_ld, v, acc);
+            sum_staged<GT, VPR>(stage, m, L, grad + grad_offset + (int64_t)(th >> ix.vshift) * D, grad_ld, v, acc);
 #pragma unroll
             for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
                         f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
         }
         __syncthreads();
-        TT* row = (TT*)tabs[th].data + (int64_t)(uint32_t)hd.z * D;
+        TT* row = (TT*)tabs[th >> ix.vshift].data + (int64_t)(uint32_t)hd.z * D;
         float* part = ix.partial + ((int64_t)th * ix.pcap + sl) * ix.pdim;
         for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
             f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -565,13 +565,13 @@ __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDes
     const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
     const int64_t off = (int64_t)t * ix.cap;
     const int64_t total = (int64_t)nchunks * D;
-    TT* table = (TT*)tabs[t].data;
+    TT* table = (TT*)tabs[t >> ix.vshift].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int cid = (int)(e / D), c = (int)(e % D);
         const int4 cd = ix.chunks[off + cid];
         float acc = 0.0f;
         for (int i = cd.x; i < cd.y; ++i)
-            acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)t * D + c]);
+            acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)(t >> ix.vshift) * D + c]);
         TT* row = table + (int64_t)(uint32_t)cd.z * D;
         row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
     }
@@ -585,13 +585,13 @@ __global__ __launch_bounds__(256) void sgd_hot_scalar(IndexerDev ix, TableDesc* 
     const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
     const int64_t off = (int64_t)t * ix.cap;
     const int64_t total = (int64_t)nhot * D;
-    TT* table = (TT*)tabs[t].data;
+    TT* table = (TT*)tabs[t >> ix.vshift].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int h = (int)(e / D), c = (int)(e % D);
         const int4 hd = ix.hot[off + h];
         float acc = 0.0f;
         for (int i = hd.x; i < hd.y; ++i)
-            acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)t * D + c]);
+            acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)(t >> ix.vshift) * D + c]);
         TT* row = table + (int64_t)(uint32_t)hd.z * D;
         row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
     }
@@ -703,6 +703,7 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
                      float lr) {
     if (T_ == 0 || N == 0) return DLRM_OK;
+    T_ <<= ix.vshift;  // virtual tables (row-parity halves) of a forward-launch build
     hipStream_t s = ctx_stream(ctx);
     const int gesz = gdtype == DLRM_F32 ? 4 : 2;
     const int tesz = tdtype == DLRM_F32 ? 4 : 2;

@@ -225,6 +225,25 @@ def test_indexer_segments_bit_exact(pkg, gpu, rows, B, L, zipf):
     _assert_segments(ix, idx, B * L)
 
 
+@pytest.mark.parametrize("rows,B,zipf", [("kaggle", 2048, None), ([300, 100000, 3, 5_000_000], 2048, 1.1),
+                                         ([1, 2, 7, 0x1000001], 1000, None), ([5], 1, None)])
+def test_step_fwd_indexer_parts(pkg, gpu, rows, B, zipf):
+    """The forward launch's indexer sorts each table as parts split by the row's low bits
+    (IndexerDev::vshift); read back through dlrm_indexer_read, the parts merge into the same
+    segments a whole-table build gives."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    D = 32
+    rng = np.random.default_rng(B + 17)
+    idx = rand_indices(rng, rows, B, 1, zipf=zipf)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(rand_tables(rng, rows, D), gpu)), B, 1, lr=0.1, index_base=0)
+    assert hp.step_api
+    x = torch.randn((B, D), device=gpu)
+    hp.step_fwd(x, pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).to(gpu)))
+    torch.cuda.synchronize()
+    _assert_segments(hp.indexer, idx, B)
+
+
 def _assert_segments(ix, idx, N):
     """One segment per distinct row (segment order unspecified), holding exactly that row's
     positions in ascending order (vectorised: large-N builds have ~N segments per table)."""

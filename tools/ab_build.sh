@@ -4,7 +4,7 @@
 set -e
 REV=${1:?rev}; DIR=${2:?dir}
 rm -rf "$DIR"; mkdir -p "$DIR/r/pkg/csrc" "$DIR/r/include"
-for f in abi.cpp lookup.hip interact.hip update.hip common.hpp indexer.hpp; do
+for f in abi.cpp lookup.hip interact.hip update.hip hashindex.hip common.hpp indexer.hpp; do
   git show "$REV:dlrm.jl_amd/csrc/$f" > "$DIR/r/pkg/csrc/$f" 2>/dev/null || rm -f "$DIR/r/pkg/csrc/$f"
 done
 git show "$REV:include/dlrm_hip.h" > "$DIR/r/include/dlrm_hip.h"
