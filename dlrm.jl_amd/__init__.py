@@ -7,6 +7,7 @@ Import name: `dlrm_jl_amd` (the directory name carries a dot; see dlrm_pkg.py).
 """
 from . import _lib
 from ._lib import BoundsError, DLRMError, LibraryMissing
+from .dense import DenseMLP, DLRMModel, bce_loss, bce_loss_back, kaggle_mlp_sizes, random_mlp
 from .embedding import (DefaultStrategy, EmbeddingTableSet, PackedIndices, PreallocationStrategy, SimpleEmbedding,
                         lookup, maplookup)
 from .hotpath import HotPath
@@ -20,5 +21,6 @@ __all__ = [
     "PreallocationStrategy", "SimpleEmbedding", "lookup", "maplookup", "HotPath", "POST_INTERACTION_PAD_TO_MUL",
     "DotInteraction", "cdiv", "dot_back", "fast_vcat", "interaction_sizes", "rrule", "up_to_mul_of",
     "KAGGLE_EMBEDDING_SIZES", "TERABYTE_EMBEDDING_SIZES", "WORKLOADS", "Descent", "SparseEmbeddingUpdate",
-    "SparseIndexer", "maplookup_pullback", "update_",
+    "SparseIndexer", "maplookup_pullback", "update_", "DenseMLP", "DLRMModel", "bce_loss", "bce_loss_back",
+    "kaggle_mlp_sizes", "random_mlp",
 ]

@@ -73,6 +73,9 @@ SIGNATURES = {
     "dlrm_indexer_build": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32]),
     "dlrm_indexer_read": (_i32, [_vp, _vp, _i32, _pi64, _pi64, _pi64, _pi64, _i64]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
+    "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),
+    "dlrm_relu_bwd_bias": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),

@@ -294,6 +294,35 @@ int dlrm_scatter_rows(dlrm_ctx* ctx, int esize, int num_tables, int batch, int d
                                vec);
 }
 
+// ---------------------------------------------------------------------- dense seams
+int dlrm_bce_head(dlrm_ctx* ctx, int batch, const float* logits, int64_t logits_ld, const float* labels, float* prob,
+                  float* dlogit, float* loss, float* dbias) {
+    CHECK_ARG(ctx, "dlrm_bce_head: null ctx");
+    CHECK_ARG(batch >= 1 && logits_ld >= 1, "dlrm_bce_head: batch=%d logits_ld=%lld", batch, (long long)logits_ld);
+    CHECK_ARG(logits && labels && prob && dlogit && loss, "dlrm_bce_head: null buffer");
+    return launch_bce_head(ctx, batch, logits, logits_ld, labels, prob, dlogit, loss, dbias);
+}
+
+int dlrm_relu_bwd_bias_workspace(int batch, int n, int64_t* work_floats, int64_t* counters) {
+    if (batch < 0 || n < 0 || !work_floats || !counters) return DLRM_E_ARG;
+    *work_floats = relu_bwd_chunks(batch) * (int64_t)n;
+    *counters = relu_bwd_groups(n);
+    return DLRM_OK;
+}
+
+int dlrm_relu_bwd_bias(dlrm_ctx* ctx, int batch, int n, const float* y, int64_t y_ld, float* g, int64_t g_ld,
+                       float* dbias, float* work, unsigned* counters) {
+    CHECK_ARG(ctx, "dlrm_relu_bwd_bias: null ctx");
+    CHECK_ARG(batch >= 0 && n >= 0 && n % 4 == 0, "dlrm_relu_bwd_bias: batch=%d n=%d (n %% 4 == 0)", batch, n);
+    CHECK_ARG(y_ld >= n && g_ld >= n && y_ld % 4 == 0 && g_ld % 4 == 0, "dlrm_relu_bwd_bias: leading dimensions");
+    if (batch == 0 || n == 0) return DLRM_OK;
+    CHECK_ARG(y && g && dbias && work && counters, "dlrm_relu_bwd_bias: null buffer");
+    CHECK_ARG((uintptr_t)y % 16 == 0 && (uintptr_t)g % 16 == 0 && (uintptr_t)dbias % 16 == 0 &&
+                  (uintptr_t)work % 16 == 0,
+              "dlrm_relu_bwd_bias: buffers must be 16-B aligned");
+    return launch_relu_bwd_bias(ctx, batch, n, y, y_ld, g, g_ld, dbias, work, counters);
+}
+
 // ---------------------------------------------------------------------- interaction
 int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* x, int64_t x_ld,
                       void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {

@@ -234,6 +234,12 @@ bool step_split_supported(bool tabs_aligned16, int T, int dtype, int d, const vo
 int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                          const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
                          const OutMap& om);
+int launch_bce_head(dlrm_ctx* ctx, int B, const float* z, int64_t z_ld, const float* y, float* prob, float* dz,
+                    float* loss, float* dbias);
+int64_t relu_bwd_chunks(int B);
+int64_t relu_bwd_groups(int N);
+int launch_relu_bwd_bias(dlrm_ctx* ctx, int B, int N, const float* y, int64_t y_ld, float* g, int64_t g_ld, float* gb,
+                         float* part, unsigned* counters);
 int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const void* src, int64_t src_ld,
                         int64_t src_off, void* dst, const int64_t* dbase, const int64_t* dld, bool vec_ok);
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,

@@ -239,6 +239,22 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
                   const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,
                   float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr, unsigned flags);
 
+/* ---- dense half of the training step (the GEMMs stay on hipBLASLt) --------
+ * dlrm_bce_head: one launch for the top MLP's head after its last GEMM, replacing
+ *   Flux.sigmoid (model.jl:83-89), bce_loss (train.jl:33-41) and rrule(bce_loss) (train.jl:43-64):
+ *   prob[b] = sigmoid(logits[b * logits_ld]); *loss = mean(-y·max(log p, -100) + (y-1)·max(log(1-p), -100));
+ *   dlogit[b] = (1/B)·((1-y)/(1-p+eps) - y/(p+eps)) · p(1-p);  *dbias (may be NULL) = Σ_b dlogit[b].
+ *   fp32; deterministic (fixed reduction order).  batch >= 1.
+ * dlrm_relu_bwd_bias: the Dense(relu) pullback seam (model.jl:72-93): g[b][:] *= (y[b][:] > 0)
+ *   in place, dbias[n] = Σ_b g[b][n], in one launch.  work / counters: caller-owned scratch sized by
+ *   dlrm_relu_bwd_bias_workspace (counters zeroed once by the caller; the kernel leaves them 0).
+ *   n % 4 == 0, y, g 16-B aligned, leading dimensions % 4 == 0.  Deterministic. */
+int dlrm_bce_head(dlrm_ctx* ctx, int batch, const float* logits, int64_t logits_ld, const float* labels,
+                  float* prob, float* dlogit, float* loss, float* dbias);
+int dlrm_relu_bwd_bias_workspace(int batch, int n, int64_t* work_floats, int64_t* counters);
+int dlrm_relu_bwd_bias(dlrm_ctx* ctx, int batch, int n, const float* y, int64_t y_ld, float* g, int64_t g_ld,
+                       float* dbias, float* work, unsigned* counters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,13 @@ see /root/reference/src/data/criteo.jl:464-560):
   upd_rows_t / upd_vals_t        touched rows of `update_emb_t` (untouched rows are asserted
                  bit-identical to `emb_t` here, so only touched rows are stored)
   lr             10.0  (src/validation.jl:23-24)
+
+Dense half (the full training step), in pytorch_reference_{kind}_dense.npz:
+  input_bot (B, 13) f32, labels (B,) f32, loss () f32, mlp_top (B,) f32
+  bot_W{i} / bot_b{i}, top_W{i} / top_b{i}     MLP parameters before the step (layer i, Flux
+                 orientation W[out][in]; PyTorch `bot_l.{i}` / `top_l.{i}`)
+  upd_bot_W{i} / upd_bot_b{i}, upd_top_W{i} / upd_top_b{i}   after one Descent(10) step
+                 (PyTorch `update_bot_{2i}` / `update_top_{2i}`, validation.jl:74-123)
 """
 import json
 import os
@@ -169,8 +176,29 @@ def process(kind):
     return meta
 
 
+def process_dense(kind):
+    h = h5py.File(os.path.join(REF, f"pytorch_reference_{kind}.hdf5"), "r")
+    arrays = dict(input_bot=h["input_bot"][()].astype(np.float32),
+                  labels=h["labels"][()].reshape(-1).astype(np.float32),
+                  loss=np.float32(h["loss"][()]), mlp_top=h["mlp_top"][()].reshape(-1).astype(np.float32))
+    for short, prefix, upd in (("bot", "bot_l", "update_bot"), ("top", "top_l", "update_top")):
+        layers = sorted({k.split(".")[1] for k in h.keys() if k.startswith(prefix + ".")}, key=int)
+        for i, l in enumerate(layers):
+            for kk, suffix in (("W", "weight"), ("b", "bias")):
+                arrays[f"{short}_{kk}{i}"] = h[f"{prefix}.{l}.{suffix}"][()].astype(np.float32)
+                arrays[f"upd_{short}_{kk}{i}"] = h[f"{upd}_{2 * i}.{suffix}"][()].astype(np.float32)
+    # the bottom MLP restated reproduces the stored mlp_bottom (the hot path's x)
+    _, _, acts = mlp_forward(h, "bot_l", arrays["input_bot"].astype(np.float64), last_sigmoid=False)
+    err = float(np.abs(acts[-1] - h["mlp_bottom"][()]).max())
+    assert err < 1e-5, err
+    np.savez_compressed(os.path.join(OUT, f"pytorch_reference_{kind}_dense.npz"), **arrays)
+    return err
+
+
 if __name__ == "__main__":
     meta = {k: process(k) for k in ("single", "multi")}
+    for k in ("single", "multi"):
+        meta[k]["err_mlp_bottom"] = process_dense(k)
     with open(os.path.join(OUT, "fixtures_meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     sys.exit(0)

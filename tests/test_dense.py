@@ -1,0 +1,244 @@
+"""The full training step around the hot path: bottom/top MLPs + BCE + Descent.
+
+Golden: the reference's ref/pytorch_reference_{single,multi}.hdf5 (MLP weights, `mlp_top`, `loss`,
+`update_bot_*`, `update_top_*`, `update_emb_*`), extracted by tests/golden/make_fixtures.py and
+checked the way src/validation.jl:17-146 checks the Julia model (one Descent(10) step; Julia
+isapprox at sqrt(eps(Float32)) on every updated parameter).
+
+CPU tests pin the dense math (dlrm.jl_amd/dense.py on CPU tensors; the interaction's dx, which
+the bottom MLP's pullback needs, comes from the oracle).  GPU tests run `DLRMModel.step` whole:
+the MLPs on hipBLASLt/rocBLAS via torch, the hot path through the HIP C ABI.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+from helpers import assert_close, julia_isapprox
+
+
+@pytest.fixture(scope="module")
+def dense_golden():
+    out = {}
+    for kind in ("single", "multi"):
+        with np.load(os.path.join(GOLDEN, f"pytorch_reference_{kind}_dense.npz"), allow_pickle=False) as z:
+            out[kind] = {k: z[k] for k in z.files}
+    return out
+
+
+def _mlp(pkg, g, short, sigmoid_last, device="cpu"):
+    n = len([k for k in g if k.startswith(f"{short}_W")])
+    Ws = [torch.from_numpy(g[f"{short}_W{i}"]).to(device) for i in range(n)]
+    bs = [torch.from_numpy(g[f"{short}_b{i}"]).to(device) for i in range(n)]
+    return pkg.DenseMLP(Ws, bs, sigmoid_last=sigmoid_last)
+
+
+def _check_updates(mlp, g, short):
+    n = len(mlp.W)
+    for i in range(n):
+        for kk, got in (("W", mlp.W[i]), ("b", mlp.b[i])):
+            want = g[f"upd_{short}_{kk}{i}"]
+            orig = g[f"{short}_{kk}{i}"]
+            got = got.detach().cpu().numpy()
+            assert not np.array_equal(orig, want)  # the step moved it (validation.jl:97)
+            assert julia_isapprox(got, want), f"update_{short}_{2 * i}.{kk}: fails Julia isapprox"
+            assert julia_isapprox(orig - got, orig - want), f"{short} layer {i} {kk}: gradient differs"
+
+
+@pytest.mark.parametrize("kind", ["single", "multi"])
+def test_dense_forward_matches_golden(pkg, golden, dense_golden, kind):
+    g, gd = golden[kind], dense_golden[kind]
+    bottom = _mlp(pkg, gd, "bot", False)
+    top = _mlp(pkg, gd, "top", True)
+    x = bottom.forward(torch.from_numpy(gd["input_bot"]))
+    assert_close(x.numpy(), g["mlp_bottom"], rtol=1e-5, what="mlp_bottom")
+    p = top.forward(torch.from_numpy(g["output_interaction"])).reshape(-1)
+    assert_close(p.numpy(), gd["mlp_top"], rtol=1e-5, what="mlp_top")
+    loss = pkg.bce_loss(p, torch.from_numpy(gd["labels"]))
+    assert abs(float(loss) - float(gd["loss"])) <= 1e-5 * abs(float(gd["loss"]))
+
+
+@pytest.mark.parametrize("kind", ["single", "multi"])
+def test_dense_backward_and_descent_match_golden(pkg, golden, dense_golden, kind):
+    """validation.jl:74-123 for both MLPs; the interaction pullback between them is the oracle's."""
+    g, gd = golden[kind], dense_golden[kind]
+    lr = float(g["lr"])
+    T, N, D = g["emb"].shape
+    B, d = g["mlp_bottom"].shape
+    L = int(g["L"])
+    bottom = _mlp(pkg, gd, "bot", False)
+    top = _mlp(pkg, gd, "top", True)
+    bottom.forward(torch.from_numpy(gd["input_bot"]))
+    p = top.forward(torch.from_numpy(g["output_interaction"])).reshape(-1)
+    labels = torch.from_numpy(gd["labels"])
+    dout = top.backward(pkg.bce_loss_back(p, labels).reshape(-1, 1))
+    assert_close(dout.numpy(), g["d_output_interaction"], rtol=1e-4, what="dLoss/d(output_interaction)")
+    ys = np.zeros((B, (T + 1) * D), dtype=np.float32)
+    oracle.maplookup(list(g["emb"]), g["idx"], 0, B, L, ys, d)
+    oracle.interact_fwd(g["mlp_bottom"], ys, T + 1)
+    dx, _ = oracle.interact_bwd(np.ascontiguousarray(dout.numpy()), ys, d, T + 1)
+    bottom.backward(torch.from_numpy(dx), need_dx=False)
+    top.sgd_(lr)
+    bottom.sgd_(lr)
+    _check_updates(top, gd, "top")
+    _check_updates(bottom, gd, "bot")
+
+
+def test_bce_clamps_like_the_reference(pkg):
+    """train.jl:36-40: log terms clamped at -100; the pullback adds eps(T) (train.jl:52-58)."""
+    p = torch.tensor([0.0, 1.0, 0.5], dtype=torch.float32)
+    y = torch.tensor([1.0, 0.0, 1.0], dtype=torch.float32)
+    loss = pkg.bce_loss(p, y)
+    want = (100.0 + 100.0 + -np.log(0.5)) / 3
+    assert abs(float(loss) - want) < 1e-4
+    dp = pkg.bce_loss_back(p, y)
+    assert torch.isfinite(dp).all()
+    eps = np.finfo(np.float32).eps
+    assert abs(float(dp[2]) - (1 / 3) * (0.0 / (0.5 + eps) - 1.0 / (0.5 + eps))) < 1e-6
+
+
+def test_model_rejects_mismatched_mlps(pkg):
+    bottom, top = pkg.kaggle_mlp_sizes(16, 26)
+    assert bottom == [13, 512, 256, 16]
+    assert top == [16 + 27 * 26 // 2, 1024, 1024, 512, 256, 1]  # criteo.jl:408-433
+    with pytest.raises(ValueError):
+        pkg.DenseMLP([torch.zeros(4, 3), torch.zeros(2, 5)], [torch.zeros(4), torch.zeros(2)])
+
+
+# ---- GPU: the whole step, HIP hot path + torch MLPs ----------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["single", "multi"])
+def test_train_step_matches_pytorch_reference(pkg, gpu, golden, dense_golden, kind):
+    """src/validation.jl:17-58 on the GPU: loss, mlp_top, every MLP update and every table update."""
+    g, gd = golden[kind], dense_golden[kind]
+    T, N, D = g["emb"].shape
+    B = g["mlp_bottom"].shape[0]
+    L = int(g["L"])
+    lr = float(g["lr"])
+    bottom = _mlp(pkg, gd, "bot", False, gpu)
+    top = _mlp(pkg, gd, "top", True, gpu)
+    tables = pkg.EmbeddingTableSet([torch.from_numpy(t).to(gpu) for t in g["emb"]])
+    model = pkg.DLRMModel(bottom, tables, top, B, L, lr=lr, index_base=0)
+    idx = pkg.PackedIndices(torch.from_numpy(g["idx"]).to(torch.int32).reshape(T, B, L).to(gpu))
+    dense = torch.from_numpy(gd["input_bot"]).to(gpu)
+    labels = torch.from_numpy(gd["labels"]).to(gpu)
+    loss = model.step(dense, idx, labels)
+    torch.cuda.synchronize()
+    model.hot.check_bounds()
+    assert abs(float(loss) - float(gd["loss"])) <= 1e-5 * abs(float(gd["loss"])), (float(loss), float(gd["loss"]))
+    assert_close(model.prob.cpu().numpy(), gd["mlp_top"], rtol=1e-5, what="mlp_top")
+    _check_updates(top, gd, "top")
+    _check_updates(bottom, gd, "bot")
+    for t in range(T):
+        rows = g[f"upd_rows_{t}"]
+        got = tables[t].data.cpu().numpy()
+        assert_close(got[rows], g[f"upd_vals_{t}"], rtol=1e-5, what=f"update_emb_{t}")
+        untouched = np.setdiff1d(np.arange(N), rows)
+        assert np.array_equal(got[untouched], g["emb"][t][untouched])
+
+
+@pytest.mark.gpu
+def test_train_step_graph_replay_equals_eager(pkg, gpu):
+    """Kaggle-shaped MLPs (criteo.jl:408-433), 26 small tables, B=512: a captured step replayed
+    twice == two eager steps, bit for bit (tables, weights, loss)."""
+    torch.manual_seed(0)
+    T, D, B = 26, 16, 512
+    rows = [1000 + 37 * t for t in range(T)]
+    bsz, tsz = pkg.kaggle_mlp_sizes(D, T)
+
+    def make():
+        gen = torch.Generator(device=gpu).manual_seed(7)
+        tabs = [torch.empty((n, D), device=gpu).uniform_(-0.05, 0.05, generator=gen) for n in rows]
+        bottom = pkg.random_mlp(bsz, sigmoid_last=False, generator=gen, device=gpu)
+        top = pkg.random_mlp(tsz, sigmoid_last=True, generator=gen, device=gpu)
+        return pkg.DLRMModel(bottom, tabs, top, B, 1, lr=0.05, index_base=0)
+
+    gen = torch.Generator(device=gpu).manual_seed(11)
+    dense = torch.randn((B, 13), device=gpu, generator=gen)
+    labels = (torch.rand((B,), device=gpu, generator=gen) < 0.3).float()
+    idx = pkg.PackedIndices(torch.stack([torch.randint(0, n, (B,), device=gpu, generator=gen, dtype=torch.int32)
+                                         for n in rows]).reshape(T, B, 1).contiguous())
+    a = make()
+    la = [float(a.step(dense, idx, labels)) for _ in range(2)]
+    b = make()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            b.step(dense, idx, labels)
+    torch.cuda.current_stream().wait_stream(s)
+    lb = []
+    for _ in range(2):
+        gr.replay()
+        torch.cuda.synchronize()
+        lb.append(float(b.loss))
+    assert la == lb
+    for ta, tb in zip(a.tables, b.tables):
+        assert torch.equal(ta.data, tb.data)
+    for pa, pb in zip(a.top.params() + a.bottom.params(), b.top.params() + b.bottom.params()):
+        assert torch.equal(pa, pb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N", [(2048, 1024), (128, 16), (1000, 260), (17, 4), (4096, 512)])
+def test_relu_bwd_bias_seam(pkg, gpu, B, N):
+    """dlrm_relu_bwd_bias == threshold_backward (bit-exact) + column sums (fp32 tolerance), and
+    its last-arriver counters leave themselves at 0 (a second launch gives the same bits)."""
+    from dlrm_jl_amd.runtime import context, ptr
+    gen = torch.Generator(device=gpu).manual_seed(B + N)
+    y = torch.randn((B, N), device=gpu, generator=gen).relu_()
+    g0 = torch.randn((B, N), device=gpu, generator=gen)
+    want_g = torch.ops.aten.threshold_backward(g0, y, 0.0)
+    want_b = want_g.double().sum(0)
+    ctx = context(gpu)
+    nw, nc = ctypes.c_int64(), ctypes.c_int64()
+    assert ctx.lib.dlrm_relu_bwd_bias_workspace(B, N, ctypes.byref(nw), ctypes.byref(nc)) == 0
+    work = torch.empty(nw.value, device=gpu)
+    cnt = torch.zeros(nc.value, dtype=torch.int32, device=gpu)
+    outs = []
+    for _ in range(2):
+        g = g0.clone()
+        gb = torch.empty(N, device=gpu)
+        ctx.check(ctx.lib.dlrm_relu_bwd_bias(ctx.bind(), B, N, ptr(y), y.stride(0), ptr(g), g.stride(0), ptr(gb),
+                                             ptr(work), ptr(cnt)))
+        torch.cuda.synchronize()
+        assert torch.equal(g, want_g)
+        outs.append(gb.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert int(cnt.abs().sum()) == 0
+    assert_close(outs[0].cpu().numpy(), want_b.cpu().numpy(), rtol=1e-5, what="bias gradient")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 128, 2048, 3001])
+def test_bce_head_seam(pkg, gpu, B):
+    """dlrm_bce_head == the torch restatement of sigmoid -> bce_loss -> rrule (train.jl:33-64),
+    including saturated logits (the -100 clamp)."""
+    from dlrm_jl_amd.runtime import context, ptr
+    gen = torch.Generator(device=gpu).manual_seed(B)
+    z = torch.randn((B, 1), device=gpu, generator=gen) * 4
+    z[: min(B, 3), 0] = torch.tensor([120.0, -120.0, 0.0], device=gpu)[: min(B, 3)]
+    y = (torch.rand(B, device=gpu, generator=gen) < 0.5).float()
+    prob, dz = torch.empty(B, device=gpu), torch.empty((B, 1), device=gpu)
+    loss, db = torch.empty((), device=gpu), torch.empty(1, device=gpu)
+    ctx = context(gpu)
+    ctx.check(ctx.lib.dlrm_bce_head(ctx.bind(), B, ptr(z), z.stride(0), ptr(y), ptr(prob), ptr(dz), ptr(loss),
+                                    ptr(db)))
+    torch.cuda.synchronize()
+    zd = z.double().reshape(-1)
+    p = torch.sigmoid(zd)
+    assert_close(prob.cpu().numpy(), p.cpu().numpy(), rtol=1e-6, what="prob")
+    want_loss = float(pkg.bce_loss(p.float(), y))
+    assert abs(float(loss) - want_loss) <= 1e-5 * max(1.0, abs(want_loss))
+    # dlogit from the kernel's own prob: near saturation 1 - p is a few ulps, so one ulp of the
+    # sigmoid moves (1-p)/(1-p+eps) by O(1) — the reference's formula, not a kernel error
+    pk = prob.double()
+    want_dz = pkg.bce_loss_back(prob, y).double() * pk * (1 - pk)
+    assert_close(dz.reshape(-1).cpu().numpy(), want_dz.cpu().numpy(), rtol=1e-4, what="dlogit")
+    assert abs(float(db) - float(dz.double().sum())) <= 1e-5 * max(1e-3, float(dz.abs().sum()))
