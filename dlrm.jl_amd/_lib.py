@@ -76,6 +76,14 @@ SIGNATURES = {
     "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),
     "dlrm_relu_bwd_bias": (_i32, [_vp, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "dlrm_dac_parse_tsv": (_i32, [_vp, _i64, _vp, _i64, _pi64]),
+    "dlrm_dac_maps_create": (_i32, [_pp]),
+    "dlrm_dac_maps_destroy": (_i32, [_vp]),
+    "dlrm_dac_maps_add": (_i32, [_vp, _vp, _i64]),
+    "dlrm_dac_maps_sizes": (_i32, [_vp, _pi64]),
+    "dlrm_dac_maps_lookup": (_i32, [_vp, _i32, _u32, ctypes.POINTER(ctypes.c_uint32)]),
+    "dlrm_dac_reindex": (_i32, [_vp, _vp, _i64]),
+    "dlrm_dac_decode": (_i32, [_vp, _vp, _i32, _vp, _vp, _i64, _vp, _i32, _i64]),
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),

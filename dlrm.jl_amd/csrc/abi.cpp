@@ -323,6 +323,17 @@ int dlrm_relu_bwd_bias(dlrm_ctx* ctx, int batch, int n, const float* y, int64_t 
     return launch_relu_bwd_bias(ctx, batch, n, y, y_ld, g, g_ld, dbias, work, counters);
 }
 
+int dlrm_dac_decode(dlrm_ctx* ctx, const dlrm_dac_record* records, int batch, float* labels, float* dense,
+                    int64_t dense_ld, void* sparse, int itype, int64_t table_stride) {
+    CHECK_ARG(ctx, "dlrm_dac_decode: null ctx");
+    CHECK_ARG(batch >= 0 && dense_ld >= 13 && table_stride >= batch, "dlrm_dac_decode: batch=%d dense_ld=%lld "
+              "table_stride=%lld", batch, (long long)dense_ld, (long long)table_stride);
+    CHECK_ARG(itype == DLRM_I32 || itype == DLRM_I64, "dlrm_dac_decode: itype %d", itype);
+    CHECK_ARG(batch == 0 || (records && labels && dense && sparse), "dlrm_dac_decode: null buffer");
+    CHECK_ARG((uintptr_t)records % 4 == 0, "dlrm_dac_decode: records must be 4-B aligned");
+    return launch_dac_decode(ctx, records, batch, labels, dense, dense_ld, sparse, itype, table_stride);
+}
+
 // ---------------------------------------------------------------------- interaction
 int dlrm_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* x, int64_t x_ld,
                       void* ys, int64_t ys_ld, void* out, int64_t out_ld, int padding) {

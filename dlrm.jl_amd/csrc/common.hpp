@@ -234,6 +234,8 @@ bool step_split_supported(bool tabs_aligned16, int T, int dtype, int d, const vo
 int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                          const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
                          const OutMap& om);
+int launch_dac_decode(dlrm_ctx* ctx, const void* rec, int B, float* labels, float* dense, int64_t dense_ld,
+                      void* sparse, int itype, int64_t tstride);
 int launch_bce_head(dlrm_ctx* ctx, int B, const float* z, int64_t z_ld, const float* y, float* prob, float* dz,
                     float* loss, float* dbias);
 int64_t relu_bwd_chunks(int B);

@@ -255,6 +255,36 @@ int dlrm_relu_bwd_bias_workspace(int batch, int n, int64_t* work_floats, int64_t
 int dlrm_relu_bwd_bias(dlrm_ctx* ctx, int batch, int n, const float* y, int64_t y_ld, float* g, int64_t g_ld,
                        float* dbias, float* work, unsigned* counters);
 
+/* ---- Criteo DAC data path (SURVEY §8 rows f2 + f4; criteo.jl:85-344) ----------------------
+ * dlrm_dac_record: DACRecord (criteo.jl:91-95), 160 bytes, the binary file format (mmap-able).
+ * dlrm_dac_parse_tsv: parseline over a buffer of TSV lines (criteo.jl:164-176): label Int32,
+ *   13 x logtransform(emptyparse(Int32, base 10)) as Float32, 26 x emptyparse(UInt32, base 16).
+ *   Blank lines are skipped; *count = records written.  DLRM_E_NOMEM if more than cap lines,
+ *   DLRM_E_ARG on a malformed line.  Host only.
+ * dlrm_dac_maps_*: categorical_values + reindex/reindex! (criteo.jl:182-262): per feature, ids
+ *   1, 2, ... in first-appearance order, accumulated over shards added in order.  Host only.
+ * dlrm_dac_reindex: reindex!(data, maps) in place (criteo.jl:251-259); DLRM_E_INDEX for a value
+ *   that is not in the maps (the reference's KeyError).
+ * dlrm_dac_decode: load! (criteo.jl:284-307) on the device: `batch` contiguous records already in
+ *   HBM -> labels [batch] f32, dense [batch][13] f32 (row stride dense_ld), sparse [26][batch]
+ *   indices (itype DLRM_I32 / DLRM_I64, table stride table_stride) = DACLoader's
+ *   Matrix{UInt32}(B, 26) layout, which is the hot path's [T][B] index layout (index_base 1). */
+typedef struct {
+    int32_t label;
+    float continuous[13];
+    uint32_t categorical[26];
+} dlrm_dac_record;
+typedef struct dlrm_dac_maps dlrm_dac_maps;
+int dlrm_dac_parse_tsv(const char* text, int64_t len, dlrm_dac_record* out, int64_t cap, int64_t* count);
+int dlrm_dac_maps_create(dlrm_dac_maps** out);
+int dlrm_dac_maps_destroy(dlrm_dac_maps* maps);
+int dlrm_dac_maps_add(dlrm_dac_maps* maps, const dlrm_dac_record* records, int64_t count);
+int dlrm_dac_maps_sizes(const dlrm_dac_maps* maps, int64_t* sizes /* [26] */);
+int dlrm_dac_maps_lookup(const dlrm_dac_maps* maps, int feature, uint32_t value, uint32_t* id);
+int dlrm_dac_reindex(const dlrm_dac_maps* maps, dlrm_dac_record* records, int64_t count);
+int dlrm_dac_decode(dlrm_ctx* ctx, const dlrm_dac_record* records, int batch, float* labels, float* dense,
+                    int64_t dense_ld, void* sparse, int itype, int64_t table_stride);
+
 #ifdef __cplusplus
 }
 #endif
