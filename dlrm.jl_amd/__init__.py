@@ -9,7 +9,7 @@ from . import _lib
 from ._lib import BoundsError, DLRMError, LibraryMissing
 from . import dac
 from .dac import DAC_DTYPE, DACLoader, DACMaps
-from .dense import DenseMLP, DLRMModel, bce_loss, bce_loss_back, kaggle_mlp_sizes, random_mlp
+from .dense import DenseMLP, DLRMModel, ShardedDLRMModel, bce_loss, bce_loss_back, kaggle_mlp_sizes, random_mlp
 from .embedding import (DefaultStrategy, EmbeddingTableSet, PackedIndices, PreallocationStrategy, SimpleEmbedding,
                         lookup, maplookup)
 from .hotpath import HotPath
@@ -24,5 +24,5 @@ __all__ = [
     "DotInteraction", "cdiv", "dot_back", "fast_vcat", "interaction_sizes", "rrule", "up_to_mul_of",
     "KAGGLE_EMBEDDING_SIZES", "TERABYTE_EMBEDDING_SIZES", "WORKLOADS", "Descent", "SparseEmbeddingUpdate",
     "SparseIndexer", "maplookup_pullback", "update_", "DenseMLP", "DLRMModel", "bce_loss", "bce_loss_back",
-    "kaggle_mlp_sizes", "random_mlp", "dac", "DAC_DTYPE", "DACLoader", "DACMaps",
+    "kaggle_mlp_sizes", "random_mlp", "dac", "DAC_DTYPE", "DACLoader", "DACMaps", "ShardedDLRMModel",
 ]

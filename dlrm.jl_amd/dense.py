@@ -23,6 +23,7 @@ import ctypes
 import math
 
 import torch
+import torch.distributed as dist
 
 from . import _lib
 
@@ -59,6 +60,22 @@ class DenseMLP:
         self._logits = False
         self._ws = {}  # (layer, batch) -> dlrm_relu_bwd_bias scratch
         self._context = None
+
+    def flatten_grads(self):
+        """Re-homes every weight/bias gradient as a view of ONE flat fp32 buffer (returned), so a
+        data-parallel step all-reduces the MLP's gradients as one bucket."""
+        def padded(k):  # every piece starts 16-B aligned (dlrm_relu_bwd_bias writes gb in float4s)
+            return (k + 3) // 4 * 4
+
+        n = sum(padded(g.numel()) for g in self.gW + self.gb)
+        flat = torch.zeros(n, dtype=torch.float32, device=self.W[0].device)
+        o = 0
+        for lst in (self.gW, self.gb):
+            for i, g in enumerate(lst):
+                lst[i] = flat[o:o + g.numel()].view(g.shape)
+                o += padded(g.numel())
+        self.flat_grad = flat
+        return flat
 
     @property
     def sizes(self):
@@ -234,3 +251,75 @@ def random_mlp(sizes, *, sigmoid_last, generator=None, device=None):
     Ws = [glorot_normal(o, i, generator, device) for i, o in zip(sizes[:-1], sizes[1:])]
     bs = [torch.zeros(o, dtype=torch.float32, device=device) for o in sizes[1:]]
     return DenseMLP(Ws, bs, sigmoid_last=sigmoid_last)
+
+
+class ShardedDLRMModel:
+    """The full training step on one rank of a table-sharded, data-parallel job (SURVEY §8 rows
+    f1 + f3): the MLPs are replicated (data parallel, B samples per rank), the tables are sharded
+    by table (`sharded.ShardedHotPath`: one all-to-all each way), and the MLP gradients are summed
+    over ranks with all-reduce (RCCL over xGMI for backend "nccl").
+
+    The loss is the global-batch mean, as one process on the world*B batch would compute it
+    (train.jl:33-41): dLoss/dlogit carries 1/(world*B), so the summed dense gradients and the
+    tables' updates equal the single-process step.  Two gradient buckets: the top MLP's is
+    all-reduced asynchronously while the sparse backward (exchange + table update) runs, the
+    bottom MLP's after its backward.  Descent(lr) then runs on every rank's replica.
+    """
+
+    def __init__(self, bottom, top, engine, lr, group=None):
+        self.bottom, self.top, self.engine = bottom, top, engine
+        self.lr = float(lr)
+        self.group = group
+        self.world = engine.world
+        self.tdtype = engine.out.dtype
+        self._top_flat = top.flatten_grads()
+        self._bot_flat = bottom.flatten_grads()
+        self.loss = None
+        self.prob = None
+
+    def _head(self, z, labels):
+        scale = 1.0 / self.world
+        if z.is_cuda:
+            B = z.shape[0]
+            if self.prob is None or self.prob.shape[0] != B:
+                self.prob = torch.empty(B, dtype=torch.float32, device=z.device)
+                self.loss = torch.empty((), dtype=torch.float32, device=z.device)
+                self._dz = torch.empty((B, 1), dtype=torch.float32, device=z.device)
+            ctx = self.top._ctx()
+            ctx.check(ctx.lib.dlrm_bce_head(ctx.bind(), B, ptr(z), z.stride(0), ptr(labels), ptr(self.prob),
+                                            ptr(self._dz), ptr(self.loss), ptr(self.top.gb[-1])))
+            if self.world > 1:
+                self._dz.mul_(scale)
+                self.top.gb[-1].mul_(scale)
+            return self._dz
+        # CPU tensors (the gloo tests): the same formulas in torch
+        p = torch.sigmoid(z).reshape(-1)
+        self.prob = p
+        self.loss = bce_loss(p, labels)
+        dz = (bce_loss_back(p, labels) * p * (1.0 - p) * scale).reshape(-1, 1)
+        self.top.gb[-1].copy_(dz.sum(0))
+        return dz
+
+    def step(self, dense, idx, labels):
+        """dense [B][13] and labels [B] of this rank's samples; idx: PackedIndices of this rank's
+        tables for the GLOBAL batch (ShardedHotPath's convention).  Returns the global-batch loss
+        (a device scalar; the all-reduce is queued, not waited on by the host)."""
+        x = self.bottom.forward(dense)
+        out = self.engine.forward(x.to(self.tdtype), idx)
+        z = self.top.forward(out.float(), logits=True)
+        dz = self._head(z, labels)
+        dout = self.top.backward(dz)
+        multi = self.world > 1
+        w_top = dist.all_reduce(self._top_flat, group=self.group, async_op=True) if multi else None
+        dx = self.engine.backward(idx, dout.to(self.tdtype).contiguous(), x)
+        self.bottom.backward(dx, need_dx=False)
+        if multi:
+            dist.all_reduce(self._bot_flat, group=self.group)
+            w_top.wait()
+        self.top.sgd_(self.lr)
+        self.bottom.sgd_(self.lr)
+        loss = self.loss.detach().clone().reshape(1)
+        if multi:
+            dist.all_reduce(loss, group=self.group)
+            loss /= self.world
+        return loss.reshape(())

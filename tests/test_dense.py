@@ -242,3 +242,87 @@ def test_bce_head_seam(pkg, gpu, B):
     want_dz = pkg.bce_loss_back(prob, y).double() * pk * (1 - pk)
     assert_close(dz.reshape(-1).cpu().numpy(), want_dz.cpu().numpy(), rtol=1e-4, what="dlogit")
     assert abs(float(db) - float(dz.double().sum())) <= 1e-5 * max(1e-3, float(dz.abs().sum()))
+
+
+def _dp_full_worker(rank, world, port, outdir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
+    dev = torch.device("cuda:0")
+    tabs, idx, dense, labels, mk = _dp_problem(pkg, dev, world)
+    T, B, D = len(tabs), dense.shape[0] // world, tabs[0].shape[1]
+    part = TablePartition(T, world)
+    mine = part.tables(rank)
+    ops = HipShardOps([torch.from_numpy(tabs[t]).to(dev) for t in mine], B * world, 1, 0.2, device=dev)
+    eng = ShardedHotPath(ops, part, rank, B, D, 1, torch.float32, dev)
+    bottom, top = mk()
+    model = pkg.ShardedDLRMModel(bottom, top, eng, 0.2)
+    p = pkg.PackedIndices(torch.from_numpy(idx[mine]).to(torch.int32).reshape(len(mine), B * world, 1).to(dev))
+    sl = slice(rank * B, (rank + 1) * B)
+    loss = model.step(torch.from_numpy(dense[sl]).to(dev), p, torch.from_numpy(labels[sl]).to(dev))
+    torch.cuda.synchronize()
+    ops.ctx.check_bounds()
+    arrs = {f"t{t}": ops.ts[k].data.cpu().numpy() for k, t in enumerate(mine)}
+    for name, m in (("bot", bottom), ("top", top)):
+        for i in range(len(m.W)):
+            arrs[f"{name}_W{i}"] = m.W[i].cpu().numpy()
+            arrs[f"{name}_b{i}"] = m.b[i].cpu().numpy()
+    np.savez(os.path.join(outdir, f"dp{rank}.npz"), loss=float(loss), **arrs)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _dp_problem(pkg, dev, world):
+    rng = np.random.default_rng(17)
+    rows, D, B = [4, 3000, 90, 60000, 13, 700], 16, 96
+    T = len(rows)
+    tabs = [rng.uniform(-0.3, 0.3, (n, D)).astype(np.float32) for n in rows]
+    idx = np.stack([rng.integers(0, n, B * world) for n in rows]).astype(np.int64)
+    dense = rng.standard_normal((B * world, 13)).astype(np.float32)
+    labels = (rng.random(B * world) < 0.3).astype(np.float32)
+    bsz, tsz = pkg.kaggle_mlp_sizes(D, T)
+
+    def mk():
+        gen = torch.Generator(device=dev).manual_seed(99)
+        return (pkg.random_mlp(bsz, sigmoid_last=False, generator=gen, device=dev),
+                pkg.random_mlp(tsz, sigmoid_last=True, generator=gen, device=dev))
+    return tabs, idx, dense, labels, mk
+
+
+@pytest.mark.gpu
+def test_data_parallel_full_step_two_ranks_equals_single_gpu(pkg, gpu, tmp_path):
+    """SURVEY rows f1 + f3: two ranks sharing the GPU (gloo; RCCL on a full node) run the full step
+    with data-parallel MLPs (bucketed gradient all-reduce) and table-sharded HIP hot path; the
+    result equals one GPU's DLRMModel on the global batch (fp32 tolerance: the dense gradients
+    are summed in a different order)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    mp.start_processes(_dp_full_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method="spawn")
+    tabs, idx, dense, labels, mk = _dp_problem(pkg, gpu, world)
+    T, Bg = len(tabs), dense.shape[0]
+    bottom, top = mk()
+    model = pkg.DLRMModel(bottom, [torch.from_numpy(t).to(gpu) for t in tabs], top, Bg, 1, lr=0.2, index_base=0)
+    p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(T, Bg, 1).to(gpu))
+    loss = float(model.step(torch.from_numpy(dense).to(gpu), p, torch.from_numpy(labels).to(gpu)))
+    from dlrm_jl_amd.sharded import TablePartition
+    part = TablePartition(T, world)
+    for r in range(world):
+        z = np.load(tmp_path / f"dp{r}.npz")
+        assert abs(float(z["loss"]) - loss) <= 1e-5 * abs(loss)
+        for name, m in (("bot", bottom), ("top", top)):
+            for i in range(len(m.W)):
+                assert_close(z[f"{name}_W{i}"], m.W[i].cpu().numpy(), rtol=1e-5, what=f"rank {r} {name} W{i}")
+                assert_close(z[f"{name}_b{i}"], m.b[i].cpu().numpy(), rtol=1e-5, what=f"rank {r} {name} b{i}")
+        for t in part.tables(r):
+            assert_close(z[f"t{t}"], model.tables[t].data.cpu().numpy(), rtol=1e-5, what=f"rank {r} table {t}")

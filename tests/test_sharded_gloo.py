@@ -166,3 +166,93 @@ def test_partition_fits_terabyte_tables():
     assert max(p2.bytes_per_rank(rows, rb)) < 240e9
     with pytest.raises(ValueError):
         TablePartition(3, 2, [[0, 1], [1, 2]])
+
+
+# ---- the full training step, data-parallel MLPs + sharded tables (SURVEY §8 rows f1 + f3) ------
+
+def _full_problem(T, rows, D, B, world, seed=11):
+    rng = np.random.default_rng(seed)
+    tables = [rng.uniform(-0.5, 0.5, size=(rows[t], D)).astype(np.float32) for t in range(T)]
+    Bg = B * world
+    idx = np.stack([rng.integers(0, rows[t], size=Bg) for t in range(T)]).astype(np.int64)
+    dense = rng.standard_normal((Bg, 13)).astype(np.float32)
+    labels = (rng.random(Bg) < 0.4).astype(np.float32)
+    F = T + 1
+    bsz = [13, 32, D]
+    tsz = [D + F * (F - 1) // 2, 24, 1]
+
+    def mlp(sizes):
+        return ([rng.standard_normal((o, i)).astype(np.float32) * np.float32((2.0 / (i + o)) ** 0.5)
+                 for i, o in zip(sizes[:-1], sizes[1:])],
+                [rng.standard_normal(o).astype(np.float32) * np.float32(0.1) for o in sizes[1:]])
+    return tables, idx, dense, labels, mlp(bsz), mlp(tsz)
+
+
+def _full_worker(rank, world, port, cfg, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    from dlrm_jl_amd.sharded import ShardedHotPath, TablePartition
+    T, rows, D, B, lr = cfg
+    tables, idx, dense, labels, (bW, bb), (tW, tb) = _full_problem(T, rows, D, B, world)
+    part = TablePartition(T, world)
+    mine = part.tables(rank)
+    ops = OracleShardOps([tables[t].copy() for t in mine], lr)
+    eng = ShardedHotPath(ops, part, rank, B, D, 1, torch.float32, torch.device("cpu"))
+    t_ = lambda a: [torch.from_numpy(v) for v in a]  # noqa: E731
+    model = pkg.ShardedDLRMModel(pkg.DenseMLP(t_(bW), t_(bb)), pkg.DenseMLP(t_(tW), t_(tb), sigmoid_last=True),
+                                 eng, lr)
+    p = pkg.PackedIndices(torch.from_numpy(idx[mine]).reshape(len(mine), B * world, 1))
+    sl = slice(rank * B, (rank + 1) * B)
+    loss = model.step(torch.from_numpy(dense[sl]).contiguous(), p, torch.from_numpy(labels[sl]).contiguous())
+    arrs = {f"table{t}": ops.tables[k] for k, t in enumerate(mine)}
+    for name, m in (("bot", model.bottom), ("top", model.top)):
+        for i in range(len(m.W)):
+            arrs[f"{name}_W{i}"] = m.W[i].numpy()
+            arrs[f"{name}_b{i}"] = m.b[i].numpy()
+    np.savez(os.path.join(outdir, f"full{rank}.npz"), loss=float(loss), **arrs)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_full_step_equals_single_process(tmp_path, pkg, world):
+    """Data-parallel MLPs (gradients all-reduced over gloo) + table-sharded hot path == one
+    process running the full step on the global batch: loss, every MLP parameter, every table."""
+    import oracle
+    from helpers import assert_close
+    T, D, B, lr = 5, 8, 6, 0.3
+    rows = [3, 50, 200, 7, 40]
+    mp.start_processes(_full_worker, args=(world, _free_port(), (T, rows, D, B, lr), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    tables, idx, dense, labels, (bW, bb), (tW, tb) = _full_problem(T, rows, D, B, world)
+    Bg, F = B * world, T + 1
+    t_ = lambda a: [torch.from_numpy(v.copy()) for v in a]  # noqa: E731
+    bottom = pkg.DenseMLP(t_(bW), t_(bb))
+    top = pkg.DenseMLP(t_(tW), t_(tb), sigmoid_last=True)
+    x = bottom.forward(torch.from_numpy(dense)).numpy()
+    ys = np.zeros((Bg, F * D), dtype=np.float32)
+    oracle.maplookup(tables, idx, 0, Bg, 1, ys, D)
+    out = oracle.interact_fwd(x, ys, F)
+    pr = top.forward(torch.from_numpy(out)).reshape(-1)
+    lab = torch.from_numpy(labels)
+    want_loss = float(pkg.bce_loss(pr, lab))
+    dout = top.backward(pkg.bce_loss_back(pr, lab).reshape(-1, 1)).numpy()
+    dx, dt = oracle.interact_bwd(np.ascontiguousarray(dout), ys, D, F)
+    oracle.sgd_update(tables, idx, 0, Bg, 1, dt, D, lr)
+    bottom.backward(torch.from_numpy(dx), need_dx=False)
+    top.sgd_(lr)
+    bottom.sgd_(lr)
+    from dlrm_jl_amd.sharded import TablePartition
+    part = TablePartition(T, world)
+    for r in range(world):
+        z = np.load(tmp_path / f"full{r}.npz")
+        assert abs(float(z["loss"]) - want_loss) <= 1e-6 * abs(want_loss)
+        for name, m in (("bot", bottom), ("top", top)):
+            for i in range(len(m.W)):
+                assert_close(z[f"{name}_W{i}"], m.W[i].numpy(), rtol=1e-5, what=f"rank {r} {name} W{i}")
+                assert_close(z[f"{name}_b{i}"], m.b[i].numpy(), rtol=1e-5, what=f"rank {r} {name} b{i}")
+        for t in part.tables(r):
+            assert_close(z[f"table{t}"], tables[t], rtol=1e-5, what=f"rank {r} table {t}")
