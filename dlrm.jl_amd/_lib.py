@@ -55,6 +55,9 @@ SIGNATURES = {
     "dlrm_free": (_i32, [_vp, _vp]),
     "dlrm_memcpy_h2d": (_i32, [_vp, _vp, _vp, _sz]),
     "dlrm_memcpy_d2h": (_i32, [_vp, _vp, _vp, _sz]),
+    "dlrm_memcpy_h2d_async": (_i32, [_vp, _vp, _vp, _sz]),
+    "dlrm_host_register": (_i32, [_vp, _sz]),
+    "dlrm_host_unregister": (_i32, [_vp]),
     "dlrm_tables_create": (_i32, [_vp, _i32, _i32, _i32, _pp, _pi64, _pp]),
     "dlrm_tables_destroy": (_i32, [_vp]),
     "dlrm_maplookup": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _i64]),

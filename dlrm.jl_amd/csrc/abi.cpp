@@ -186,6 +186,21 @@ int dlrm_memcpy_h2d(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes) {
     return rc ? rc : ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
 }
 
+int dlrm_memcpy_h2d_async(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    CHECK_ARG(ctx && (bytes == 0 || (dst && src)), "dlrm_memcpy_h2d_async: null argument");
+    return ctx_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream), "memcpy h2d async");
+}
+
+int dlrm_host_register(void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return DLRM_E_ARG;
+    return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? DLRM_OK : DLRM_E_HIP;
+}
+
+int dlrm_host_unregister(void* ptr) {
+    if (!ptr) return DLRM_E_ARG;
+    return hipHostUnregister(ptr) == hipSuccess ? DLRM_OK : DLRM_E_HIP;
+}
+
 int dlrm_memcpy_d2h(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes) {
     CHECK_ARG(ctx && (bytes == 0 || (dst && src)), "dlrm_memcpy_d2h: null argument");
     int rc = ctx_hip(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream), "memcpy d2h");

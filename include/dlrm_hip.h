@@ -89,6 +89,12 @@ int dlrm_malloc(dlrm_ctx* ctx, size_t bytes, void** dptr);
 int dlrm_free(dlrm_ctx* ctx, void* dptr);
 int dlrm_memcpy_h2d(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes); /* synchronous */
 int dlrm_memcpy_d2h(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes); /* synchronous */
+/* Page-locks a host range for direct DMA (hipHostRegister) / releases it; dlrm_memcpy_h2d_async
+ * queues a copy on the ctx stream and returns (the source must stay unchanged until the stream
+ * reaches it; from registered memory the copy is a DMA with no staging). */
+int dlrm_host_register(void* ptr, size_t bytes);
+int dlrm_host_unregister(void* ptr);
+int dlrm_memcpy_h2d_async(dlrm_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* ---- embedding tables --------------------------------------------------------------- */
 /* Registers T tables of one dtype and feature size `dim` (SimpleEmbedding{Static{dim}}).

@@ -112,10 +112,12 @@ def reindexed(pkg, ref_records):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("itype", [torch.int32, torch.int64])
-def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype):
+@pytest.mark.parametrize("itype,direct", [(torch.int32, True), (torch.int64, True), (torch.int32, False)])
+def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype, direct):
+    """direct: the dataset page-locked, one DMA per batch; else pinned staging buffers."""
     data, _ = reindexed
-    loader = pkg.DACLoader(data, 64, gpu, index_dtype=itype)
+    loader = pkg.DACLoader(data, 64, gpu, index_dtype=itype, direct=direct)
+    assert loader.direct == direct
     assert len(loader) == 250 // 64  # whole batches only (criteo.jl:326-329)
     seen = 0
     for i, b in enumerate(loader):
@@ -125,6 +127,7 @@ def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype):
         assert np.array_equal(b.sparse.cpu().numpy(), sparse.astype(np.int64))
         seen += 1
     assert seen == 3
+    loader.close()
 
 
 @pytest.mark.gpu

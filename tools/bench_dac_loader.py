@@ -23,6 +23,7 @@ import dlrm_pkg  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=200)
+    ap.add_argument("--direct", type=int, default=0, help="1: page-locked dataset, one DMA per batch")
     a = ap.parse_args()
     pkg = dlrm_pkg.load()
     dev = torch.device("cuda:0")
@@ -35,7 +36,7 @@ def main():
     data["continuous"] = rng.random((len(data), 13), dtype=np.float32)
     data["categorical"] = np.stack([rng.integers(1, n + 1, len(data)) for n in rows], axis=1).astype(np.uint32)
 
-    loader = pkg.DACLoader(data, B, dev)
+    loader = pkg.DACLoader(data, B, dev, direct=a.direct == 1)
     for _ in loader:  # warm-up
         pass
     torch.cuda.synchronize()
@@ -73,7 +74,7 @@ def main():
         "loader_only_records_per_s": round(n / t_load, 1),
         "step_only_samples_per_s_eager": round(n / t_step, 1),
         "loader_plus_step_samples_per_s_eager": round(n / t_both, 1),
-        "batch": B, "batches": len(loader), "record_bytes": 160,
+        "batch": B, "batches": len(loader), "record_bytes": 160, "direct_dma": loader.direct,
         "loader_GBps": round(n * 160 / t_load / 1e9, 2),
         "note": "eager launches (no hipGraph): the loader's host staging runs beside the GPU step",
     }))
