@@ -87,6 +87,12 @@ SIGNATURES = {
     "dlrm_dac_maps_lookup": (_i32, [_vp, _i32, _u32, ctypes.POINTER(ctypes.c_uint32)]),
     "dlrm_dac_reindex": (_i32, [_vp, _vp, _i64]),
     "dlrm_dac_decode": (_i32, [_vp, _vp, _i32, _vp, _vp, _i64, _vp, _i32, _i64]),
+    "dlrm_dac_loader_create": (_i32, [_i32, _vp, _i64, _i32, _i32, _pp, _pp, _pp, _pp]),
+    "dlrm_dac_loader_start": (_i32, [_vp, _pi64]),
+    "dlrm_dac_loader_next": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_int)]),
+    "dlrm_dac_loader_release": (_i32, [_vp, _i32, _vp]),
+    "dlrm_dac_loader_stop": (_i32, [_vp]),
+    "dlrm_dac_loader_destroy": (_i32, [_vp]),
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),

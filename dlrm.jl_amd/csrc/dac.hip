@@ -193,3 +193,201 @@ extern "C" int dlrm_dac_reindex(const dlrm_dac_maps* m, dlrm_dac_record* recs, i
     }
     return DLRM_OK;
 }
+
+// ---------------------------------------------------------------------- native prefetching loader
+// DACLoader's iteration with a native prefetch thread: the worker copies batch i's records into
+// one of two pinned (hipHostMalloc) buffers, uploads them on the loader's own stream and decodes
+// them into the caller's slot-i&1 outputs, while the caller computes on the other slot.  The
+// caller's stream waits for a slot's `ready` event (dlrm_dac_loader_next); releasing a slot
+// records `consumed` on the caller's stream, which the worker's stream waits for before it
+// overwrites that slot.  The worker has its own dlrm_ctx (a ctx is not re-entrant).
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+struct dlrm_dac_loader {
+    int device = 0;
+    dlrm_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    const char* data = nullptr;
+    int64_t count = 0;
+    int B = 0, itype = 0;
+    void* pinned[2] = {nullptr, nullptr};
+    void* raw[2] = {nullptr, nullptr};
+    float* labels[2] = {nullptr, nullptr};
+    float* dense[2] = {nullptr, nullptr};
+    void* sparse[2] = {nullptr, nullptr};
+    hipEvent_t ready[2] = {}, consumed[2] = {}, h2d[2] = {};
+    bool consumed_valid[2] = {false, false}, h2d_valid[2] = {false, false};
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool slot_free[2] = {true, true};
+    std::deque<int> ready_q;
+    int64_t produced = 0, nbatches = 0;
+    bool stop = false, running = false;
+    int error = 0;
+};
+
+namespace {
+
+void dac_worker(dlrm_dac_loader* L) {
+    if (hipSetDevice(L->device) != hipSuccess) {
+        std::lock_guard<std::mutex> g(L->mu);
+        L->error = DLRM_E_HIP;
+        L->cv.notify_all();
+        return;
+    }
+    const size_t bytes = (size_t)L->B * sizeof(dlrm_dac_record);
+    for (int64_t i = 0; i < L->nbatches; ++i) {
+        const int slot = (int)(i & 1);
+        {
+            std::unique_lock<std::mutex> lk(L->mu);
+            L->cv.wait(lk, [&] { return L->stop || L->slot_free[slot]; });
+            if (L->stop) return;
+            L->slot_free[slot] = false;
+        }
+        int rc = DLRM_OK;
+        if (L->h2d_valid[slot] && hipEventSynchronize(L->h2d[slot]) != hipSuccess) rc = DLRM_E_HIP;
+        if (rc == DLRM_OK) {
+            memcpy(L->pinned[slot], L->data + (size_t)i * bytes, bytes);
+            if (L->consumed_valid[slot] && hipStreamWaitEvent(L->stream, L->consumed[slot], 0) != hipSuccess)
+                rc = DLRM_E_HIP;
+        }
+        if (rc == DLRM_OK && hipMemcpyAsync(L->raw[slot], L->pinned[slot], bytes, hipMemcpyHostToDevice, L->stream) !=
+                                 hipSuccess)
+            rc = DLRM_E_HIP;
+        if (rc == DLRM_OK && hipEventRecord(L->h2d[slot], L->stream) != hipSuccess) rc = DLRM_E_HIP;
+        L->h2d_valid[slot] = rc == DLRM_OK;
+        if (rc == DLRM_OK)
+            rc = dlrm::launch_dac_decode(L->ctx, L->raw[slot], L->B, L->labels[slot], L->dense[slot], 13,
+                                         L->sparse[slot], L->itype, L->B);
+        if (rc == DLRM_OK && hipEventRecord(L->ready[slot], L->stream) != hipSuccess) rc = DLRM_E_HIP;
+        std::lock_guard<std::mutex> g(L->mu);
+        if (rc != DLRM_OK) {
+            L->error = rc;
+            L->cv.notify_all();
+            return;
+        }
+        L->ready_q.push_back(slot);
+        ++L->produced;
+        L->cv.notify_all();
+    }
+}
+
+void dac_loader_join(dlrm_dac_loader* L) {
+    {
+        std::lock_guard<std::mutex> g(L->mu);
+        L->stop = true;
+        L->cv.notify_all();
+    }
+    if (L->th.joinable()) L->th.join();
+    L->running = false;
+}
+
+}  // namespace
+
+extern "C" int dlrm_dac_loader_create(int device, const dlrm_dac_record* records, int64_t count, int batch,
+                                      int itype, float* const* labels, float* const* dense, void* const* sparse,
+                                      dlrm_dac_loader** out) {
+    if (!out || batch <= 0 || count < 0 || (count > 0 && !records) || !labels || !dense || !sparse) return DLRM_E_ARG;
+    if (itype != DLRM_I32 && itype != DLRM_I64) return DLRM_E_ARG;
+    for (int k = 0; k < 2; ++k)
+        if (!labels[k] || !dense[k] || !sparse[k]) return DLRM_E_ARG;
+    dlrm_dac_loader* L = new (std::nothrow) dlrm_dac_loader();
+    if (!L) return DLRM_E_NOMEM;
+    L->device = device;
+    L->data = (const char*)records;
+    L->count = count;
+    L->B = batch;
+    L->itype = itype;
+    const size_t bytes = (size_t)batch * sizeof(dlrm_dac_record);
+    bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; ok && k < 2; ++k) {
+        L->labels[k] = labels[k];
+        L->dense[k] = dense[k];
+        L->sparse[k] = sparse[k];
+        ok = hipHostMalloc(&L->pinned[k], bytes, hipHostMallocDefault) == hipSuccess &&
+             hipMalloc(&L->raw[k], bytes) == hipSuccess &&
+             hipEventCreateWithFlags(&L->ready[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&L->consumed[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&L->h2d[k], hipEventDisableTiming) == hipSuccess;
+    }
+    if (ok) ok = dlrm_ctx_create(device, L->stream, &L->ctx) == DLRM_OK;
+    if (!ok) {
+        dlrm_dac_loader_destroy(L);
+        return DLRM_E_HIP;
+    }
+    *out = L;
+    return DLRM_OK;
+}
+
+extern "C" int dlrm_dac_loader_start(dlrm_dac_loader* L, int64_t* nbatches) {
+    if (!L) return DLRM_E_ARG;
+    dac_loader_join(L);  // a previous epoch's worker, if any
+    // the previous epoch's uploads must have left the pinned buffers / raw slots
+    if (L->stream && hipStreamSynchronize(L->stream) != hipSuccess) return DLRM_E_HIP;
+    L->stop = false;
+    L->error = 0;
+    L->ready_q.clear();
+    L->produced = 0;
+    L->slot_free[0] = L->slot_free[1] = true;
+    L->nbatches = L->count / L->B;  // whole batches only (criteo.jl:326-329)
+    if (nbatches) *nbatches = L->nbatches;
+    L->running = true;
+    L->th = std::thread(dac_worker, L);
+    return DLRM_OK;
+}
+
+extern "C" int dlrm_dac_loader_next(dlrm_dac_loader* L, void* consumer_stream, int* slot) {
+    if (!L || !slot) return DLRM_E_ARG;
+    int s;
+    {
+        std::unique_lock<std::mutex> lk(L->mu);
+        L->cv.wait(lk, [&] { return !L->ready_q.empty() || L->error || !L->running || L->produced >= L->nbatches; });
+        if (L->ready_q.empty()) {
+            if (L->error) return L->error;
+            *slot = -1;  // the epoch is over
+            return DLRM_OK;
+        }
+        s = L->ready_q.front();
+        L->ready_q.pop_front();
+    }
+    if (hipStreamWaitEvent((hipStream_t)consumer_stream, L->ready[s], 0) != hipSuccess) return DLRM_E_HIP;
+    *slot = s;
+    return DLRM_OK;
+}
+
+extern "C" int dlrm_dac_loader_release(dlrm_dac_loader* L, int slot, void* consumer_stream) {
+    if (!L || slot < 0 || slot > 1) return DLRM_E_ARG;
+    if (hipEventRecord(L->consumed[slot], (hipStream_t)consumer_stream) != hipSuccess) return DLRM_E_HIP;
+    std::lock_guard<std::mutex> g(L->mu);
+    L->consumed_valid[slot] = true;
+    L->slot_free[slot] = true;
+    L->cv.notify_all();
+    return DLRM_OK;
+}
+
+extern "C" int dlrm_dac_loader_stop(dlrm_dac_loader* L) {
+    if (!L) return DLRM_E_ARG;
+    dac_loader_join(L);
+    return DLRM_OK;
+}
+
+extern "C" int dlrm_dac_loader_destroy(dlrm_dac_loader* L) {
+    if (!L) return DLRM_OK;
+    dac_loader_join(L);
+    if (L->stream) (void)hipStreamSynchronize(L->stream);
+    if (L->ctx) dlrm_ctx_destroy(L->ctx);
+    for (int k = 0; k < 2; ++k) {
+        if (L->pinned[k]) (void)hipHostFree(L->pinned[k]);
+        if (L->raw[k]) (void)hipFree(L->raw[k]);
+        if (L->ready[k]) (void)hipEventDestroy(L->ready[k]);
+        if (L->consumed[k]) (void)hipEventDestroy(L->consumed[k]);
+        if (L->h2d[k]) (void)hipEventDestroy(L->h2d[k]);
+    }
+    if (L->stream) (void)hipStreamDestroy(L->stream);
+    delete L;
+    return DLRM_OK;
+}

@@ -151,8 +151,10 @@ class DACLoader:
     `PackedIndices` takes with index_base=1).  Only whole batches are produced:
     len = div(length(dataset), batchsize), as in the reference.
 
-    Default: each batch's records are copied into one of two pinned (hipHostMalloc) staging
-    buffers, then uploaded.  With `direct=True` the dataset's memory is page-locked once
+    Default (`native`): a C++ prefetch thread (dlrm_dac_loader_*) copies each batch's records into
+    one of two pinned (hipHostMalloc) staging buffers, uploads and decodes them on its own stream
+    while the caller computes (34.6 M samples/s beside the eager hot-path step, against 30.7 M
+    with `native=False`, where the same staging is driven from the caller's thread).  With `direct=True` the dataset's memory is page-locked once
     (dlrm_host_register) and each batch is one async DMA straight out of it (falls back to staging
     when registration is refused, e.g. a read-only file mapping or a dataset over
     DIRECT_MAX_BYTES).  Measured on MI355X (tools/bench_dac_loader.py, B = 2048): staging 53 M
@@ -165,7 +167,7 @@ class DACLoader:
     MI355X, 20.6 M records/s alone and 14.3 M samples/s beside the step, against 53 M and
     27.8-30.7 M for this single-threaded form, so staging runs in the caller's thread.)"""
 
-    def __init__(self, dataset, batchsize, device=None, *, index_dtype=torch.int32, direct=False):
+    def __init__(self, dataset, batchsize, device=None, *, index_dtype=torch.int32, direct=False, native=True):
         if dataset.dtype != DAC_DTYPE:
             raise ValueError("dataset must be a DAC_DTYPE record array (load / binarize)")
         self.dataset = dataset
@@ -190,12 +192,27 @@ class DACLoader:
         # direct DMA: the dataset itself page-locked (hipHostRegister), each batch one async copy
         # straight out of it (no host memcpy, no host wait); else the pinned staging buffers
         self._registered = None
+        self._nl = None
         nb = self._raw.nbytes
         if direct and 0 < nb <= DIRECT_MAX_BYTES and self._raw.flags.c_contiguous:
             addr = self._raw.ctypes.data
             if self.ctx.lib.dlrm_host_register(ctypes.c_void_p(addr), nb) == _lib.OK:
                 self._registered = addr
         self.direct = self._registered is not None
+        # native (default): a C++ prefetch thread stages / uploads / decodes the next batch
+        # (dlrm_dac_loader_*) while the caller computes; the Python-driven forms below remain for
+        # `direct` and for comparison
+        self._nl = None
+        if native and not self.direct and len(self) > 0:
+            dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            arr = lambda ts: (ctypes.c_void_p * 2)(*[t.data_ptr() for t in ts])  # noqa: E731
+            h = ctypes.c_void_p()
+            _lib.check(self.ctx.lib.dlrm_dac_loader_create(
+                dev_index, ctypes.c_void_p(self._raw.ctypes.data), len(dataset), self.B, self.itype,
+                arr([o.labels for o in self._out]), arr([o.dense for o in self._out]),
+                arr([o.sparse for o in self._out]), ctypes.byref(h)))
+            self._nl = h
+        self.native = self._nl is not None
 
     def __len__(self):
         return len(self.dataset) // self.B
@@ -226,8 +243,31 @@ class DACLoader:
                                                         self.itype, out.sparse.stride(0)))
             self._ready[slot].record(self._copy)
 
+    def _iter_native(self, cur):
+        lib = self.ctx.lib
+        _lib.check(lib.dlrm_dac_loader_start(self._nl, None))
+        st = ctypes.c_void_p(cur.cuda_stream)
+        held = -1
+        try:
+            while True:
+                slot = ctypes.c_int()
+                _lib.check(lib.dlrm_dac_loader_next(self._nl, st, ctypes.byref(slot)))
+                if slot.value < 0:
+                    return
+                held = slot.value
+                yield self._out[held]
+                _lib.check(lib.dlrm_dac_loader_release(self._nl, held, st))  # the caller's work is queued
+                held = -1
+        finally:
+            if held >= 0:
+                lib.dlrm_dac_loader_release(self._nl, held, st)
+            lib.dlrm_dac_loader_stop(self._nl)
+
     def close(self):
-        """Releases the page-locked dataset (after the queued copies have run)."""
+        """Releases the page-locked dataset (after the queued copies have run) and the native loader."""
+        if self._nl is not None:
+            self.ctx.lib.dlrm_dac_loader_destroy(self._nl)
+            self._nl = None
         if self._registered is not None:
             self._copy.synchronize()
             self.ctx.lib.dlrm_host_unregister(ctypes.c_void_p(self._registered))
@@ -245,6 +285,9 @@ class DACLoader:
         if n == 0:
             return
         cur = torch.cuda.current_stream(self.device)
+        if self._nl is not None:
+            yield from self._iter_native(cur)
+            return
         self._stage(0, 0, wait_consumer=False)
         for i in range(n):
             slot = i & 1

@@ -290,6 +290,22 @@ int dlrm_dac_maps_lookup(const dlrm_dac_maps* maps, int feature, uint32_t value,
 int dlrm_dac_reindex(const dlrm_dac_maps* maps, dlrm_dac_record* records, int64_t count);
 int dlrm_dac_decode(dlrm_ctx* ctx, const dlrm_dac_record* records, int batch, float* labels, float* dense,
                     int64_t dense_ld, void* sparse, int itype, int64_t table_stride);
+/* Native prefetching DACLoader.  create: `records` (host, count records, kept alive by the
+ * caller) and the caller's two output slots (device: labels[k] [batch] f32, dense[k] [batch][13]
+ * f32, sparse[k] [26][batch] of itype).  start: one epoch of count/batch whole batches on a
+ * native worker thread (pinned staging, upload + dlrm_dac_decode on the loader's own stream).
+ * next: blocks until the next batch is decoded, makes consumer_stream wait for it, returns its
+ * slot (-1: epoch over).  release: the caller's work on that slot is queued on consumer_stream;
+ * the slot may be refilled after it.  stop: ends the epoch early.  The calls for one loader
+ * come from one host thread. */
+typedef struct dlrm_dac_loader dlrm_dac_loader;
+int dlrm_dac_loader_create(int device, const dlrm_dac_record* records, int64_t count, int batch, int itype,
+                           float* const* labels, float* const* dense, void* const* sparse, dlrm_dac_loader** out);
+int dlrm_dac_loader_start(dlrm_dac_loader* loader, int64_t* nbatches);
+int dlrm_dac_loader_next(dlrm_dac_loader* loader, void* consumer_stream, int* slot);
+int dlrm_dac_loader_release(dlrm_dac_loader* loader, int slot, void* consumer_stream);
+int dlrm_dac_loader_stop(dlrm_dac_loader* loader);
+int dlrm_dac_loader_destroy(dlrm_dac_loader* loader);
 
 #ifdef __cplusplus
 }

@@ -112,12 +112,20 @@ def reindexed(pkg, ref_records):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("itype,direct", [(torch.int32, True), (torch.int64, True), (torch.int32, False)])
-def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype, direct):
-    """direct: the dataset page-locked, one DMA per batch; else pinned staging buffers."""
+@pytest.mark.parametrize("itype,direct,native", [(torch.int32, False, True), (torch.int64, False, True),
+                                                 (torch.int32, True, False), (torch.int32, False, False)])
+def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype, direct, native):
+    """native: the C++ prefetch thread; direct: the dataset page-locked, one DMA per batch; else
+    pinned staging driven from Python.  Two epochs (the loader restarts), the second one
+    abandoned after one batch and then a third run in full."""
     data, _ = reindexed
-    loader = pkg.DACLoader(data, 64, gpu, index_dtype=itype, direct=direct)
-    assert loader.direct == direct
+    loader = pkg.DACLoader(data, 64, gpu, index_dtype=itype, direct=direct, native=native)
+    assert loader.direct == direct and loader.native == native
+    for b in loader:  # an epoch, then an abandoned one
+        pass
+    it = iter(loader)
+    next(it)
+    it.close()
     assert len(loader) == 250 // 64  # whole batches only (criteo.jl:326-329)
     seen = 0
     for i, b in enumerate(loader):
