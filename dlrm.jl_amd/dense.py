@@ -58,24 +58,35 @@ class DenseMLP:
         self.gb = [torch.zeros_like(b) for b in self.b]
         self._acts = None  # [input, a_1, ..., a_n] of the last forward
         self._logits = False
+        self.flat_param = self.flat_grad = None
         self._ws = {}  # (layer, batch) -> dlrm_relu_bwd_bias scratch
         self._context = None
 
-    def flatten_grads(self):
-        """Re-homes every weight/bias gradient as a view of ONE flat fp32 buffer (returned), so a
-        data-parallel step all-reduces the MLP's gradients as one bucket."""
-        def padded(k):  # every piece starts 16-B aligned (dlrm_relu_bwd_bias writes gb in float4s)
+    def flatten(self):
+        """Re-homes every weight/bias AND its gradient as views of two flat fp32 buffers with the
+        same piece offsets (every piece 16-B aligned: dlrm_relu_bwd_bias writes gb in float4s).
+        The Descent step is then one axpy launch over the whole MLP, and a data-parallel step
+        all-reduces the gradients as one bucket (the returned flat gradient)."""
+        if self.flat_grad is not None:
+            return self.flat_grad
+
+        def padded(k):
             return (k + 3) // 4 * 4
 
         n = sum(padded(g.numel()) for g in self.gW + self.gb)
-        flat = torch.zeros(n, dtype=torch.float32, device=self.W[0].device)
+        dev = self.W[0].device
+        fp = torch.zeros(n, dtype=torch.float32, device=dev)
+        fg = torch.zeros(n, dtype=torch.float32, device=dev)
         o = 0
-        for lst in (self.gW, self.gb):
-            for i, g in enumerate(lst):
-                lst[i] = flat[o:o + g.numel()].view(g.shape)
-                o += padded(g.numel())
-        self.flat_grad = flat
-        return flat
+        for plist, glist in ((self.W, self.gW), (self.b, self.gb)):
+            for i in range(len(plist)):
+                k = plist[i].numel()
+                fp[o:o + k].copy_(plist[i].reshape(-1))
+                plist[i] = fp[o:o + k].view(plist[i].shape)
+                glist[i] = fg[o:o + k].view(glist[i].shape)
+                o += padded(k)
+        self.flat_param, self.flat_grad = fp, fg
+        return fg
 
     @property
     def sizes(self):
@@ -152,8 +163,13 @@ class DenseMLP:
         return g if need_dx else None
 
     def sgd_(self, lr):
-        """Flux.update!(Descent(η), p, g) for every weight and bias (train.jl:251-271)."""
-        torch._foreach_add_(self.params(), self.grads(), alpha=-float(lr))
+        """Flux.update!(Descent(η), p, g) for every weight and bias (train.jl:251-271): one launch
+        over the flat buffers after `flatten`, else one multi-tensor launch.  (The padding between
+        pieces holds zero gradients, so it stays zero.)"""
+        if self.flat_param is not None:
+            self.flat_param.add_(self.flat_grad, alpha=-float(lr))
+        else:
+            torch._foreach_add_(self.params(), self.grads(), alpha=-float(lr))
 
 
 def bce_loss(p, labels):
@@ -194,6 +210,8 @@ class DLRMModel:
         self.tdtype = ts.dtype
         self.loss = None
         self.prob = None
+        bottom.flatten()  # one Descent launch per MLP
+        top.flatten()
 
     @property
     def tables(self):
@@ -272,8 +290,8 @@ class ShardedDLRMModel:
         self.group = group
         self.world = engine.world
         self.tdtype = engine.out.dtype
-        self._top_flat = top.flatten_grads()
-        self._bot_flat = bottom.flatten_grads()
+        self._top_flat = top.flatten()
+        self._bot_flat = bottom.flatten()
         self.loss = None
         self.prob = None
 
