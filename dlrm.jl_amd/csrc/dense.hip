@@ -6,6 +6,8 @@
 //   relu_bwd_bias_kernel relu pullback (g .* (y .> 0)) fused with the bias gradient Σ_b g[b, :]
 //                        (Flux Dense pullback, model.jl:72-93)
 // Both reduce in a fixed order (deterministic: replaying a step gives the same bits).
+#include <stdlib.h>
+
 #include "common.hpp"
 
 namespace dlrm {
@@ -164,6 +166,80 @@ relu_bwd_bias_kernel(int B, int N, const float* __restrict__ yv, int64_t y_ld, f
     }
 }
 
+// Two-launch form of the same seam (the default; DLRM_RELU_2PASS=0 selects the one-launch form above): launch A masks
+// g and writes the 16-row column sums to part[chunk][N] with plain stores; launch B (after the
+// kernel boundary: no fences, no counters) sums the chunks per column in chunk order.
+__global__ void __launch_bounds__(kReluThreads)
+relu_mask_partial_kernel(int B, int N, const float* __restrict__ yv, int64_t y_ld, float* __restrict__ g,
+                         int64_t g_ld, float* __restrict__ part) {
+    __shared__ float4 sacc[kReluThreads / kWave][kWave];
+    constexpr int U = 4;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int c = (blockIdx.x * kWave + lane) * 4;
+    const bool col_ok = c < N;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int r0 = blockIdx.y * kReluRows + w * kReluWaveRows;
+    if (col_ok) {
+        for (int k0 = 0; k0 < kReluWaveRows; k0 += U) {
+            float4 gg[U], yy[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = min(r0 + k0 + u, B - 1);
+                gg[u] = ldg<float4>(g + (int64_t)r * g_ld + c);
+                yy[u] = ldg<float4>(yv + (int64_t)r * y_ld + c);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = r0 + k0 + u;
+                if (r < B) {
+                    gg[u].x = yy[u].x > 0.f ? gg[u].x : 0.f;
+                    gg[u].y = yy[u].y > 0.f ? gg[u].y : 0.f;
+                    gg[u].z = yy[u].z > 0.f ? gg[u].z : 0.f;
+                    gg[u].w = yy[u].w > 0.f ? gg[u].w : 0.f;
+                    stg<float4>(g + (int64_t)r * g_ld + c, gg[u]);
+                    add4(acc, gg[u]);
+                }
+            }
+        }
+    }
+    sacc[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int k = 1; k < kReluThreads / kWave; ++k) add4(acc, sacc[k][lane]);
+        if (col_ok) stg<float4>(part + (int64_t)blockIdx.y * N + c, acc);
+    }
+}
+
+// 64 columns per workgroup: 16 column lanes (float4) x 16 chunk lanes; chunk lane q sums chunks
+// q, q+16, ... (8 loads in flight), then lane q = 0 adds the 16 partial sums in q order.
+__global__ void __launch_bounds__(256)
+colsum_chunks_kernel(int nch, int N, const float* __restrict__ part, float* __restrict__ gb) {
+    __shared__ float4 s[16][16];
+    constexpr int UC = 8;
+    const int cq = threadIdx.x & 15, q = threadIdx.x >> 4;
+    const int c = blockIdx.x * 64 + cq * 4;
+    const bool col_ok = c < N;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col_ok) {
+        for (int k0 = q; k0 < nch; k0 += 16 * UC) {
+            float4 a[UC];
+#pragma unroll
+            for (int u = 0; u < UC; ++u) a[u] = ldg<float4>(part + (int64_t)min(k0 + u * 16, nch - 1) * N + c);
+#pragma unroll
+            for (int u = 0; u < UC; ++u)
+                if (k0 + u * 16 < nch) add4(acc, a[u]);
+        }
+    }
+    s[q][cq] = acc;
+    __syncthreads();
+    if (q == 0 && col_ok) {
+#pragma unroll
+        for (int k = 1; k < 16; ++k) add4(acc, s[k][cq]);
+        stg<float4>(gb + c, acc);
+    }
+}
+
 int launch_bce_head(dlrm_ctx* ctx, int B, const float* z, int64_t z_ld, const float* y, float* prob, float* dz,
                     float* loss, float* dbias) {
     hipLaunchKernelGGL(bce_head_kernel, dim3(1), dim3(kHeadThreads), 0, ctx_stream(ctx), B, z, z_ld, y, prob, dz, loss,
@@ -178,6 +254,16 @@ int launch_relu_bwd_bias(dlrm_ctx* ctx, int B, int N, const float* y, int64_t y_
                          float* part, unsigned* counters) {
     if (B == 0 || N == 0) return DLRM_OK;
     const dim3 grid((unsigned)relu_bwd_groups(N), (unsigned)relu_bwd_chunks(B));
+    // default: the two-launch form (full step 483 vs 504-509 us with the last-arriver form on MI355X);
+    // DLRM_RELU_2PASS=0 selects the one-launch last-arriver form
+    static const bool two_pass = !(getenv("DLRM_RELU_2PASS") && atoi(getenv("DLRM_RELU_2PASS")) == 0);
+    if (two_pass) {
+        hipLaunchKernelGGL(relu_mask_partial_kernel, grid, dim3(kReluThreads), 0, ctx_stream(ctx), B, N, y, y_ld, g,
+                           g_ld, part);
+        hipLaunchKernelGGL(colsum_chunks_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, ctx_stream(ctx),
+                           (int)relu_bwd_chunks(B), N, (const float*)part, gb);
+        return ctx_hip(ctx, hipGetLastError(), "relu_bwd_bias (two-pass) launch");
+    }
     hipLaunchKernelGGL(relu_bwd_bias_kernel, grid, dim3(kReluThreads), 0, ctx_stream(ctx), B, N, y, y_ld, g, g_ld, gb,
                        part, counters);
     return ctx_hip(ctx, hipGetLastError(), "relu_bwd_bias launch");

@@ -252,7 +252,8 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
  *   dlogit[b] = (1/B)·((1-y)/(1-p+eps) - y/(p+eps)) · p(1-p);  *dbias (may be NULL) = Σ_b dlogit[b].
  *   fp32; deterministic (fixed reduction order).  batch >= 1.
  * dlrm_relu_bwd_bias: the Dense(relu) pullback seam (model.jl:72-93): g[b][:] *= (y[b][:] > 0)
- *   in place, dbias[n] = Σ_b g[b][n], in one launch.  work / counters: caller-owned scratch sized by
+ *   in place, dbias[n] = Σ_b g[b][n] (two launches: mask + 16-row column sums, then the column
+ *   sums of those in chunk order).  work / counters: caller-owned scratch sized by
  *   dlrm_relu_bwd_bias_workspace (counters zeroed once by the caller; the kernel leaves them 0).
  *   n % 4 == 0, y, g 16-B aligned, leading dimensions % 4 == 0.  Deterministic. */
 int dlrm_bce_head(dlrm_ctx* ctx, int batch, const float* logits, int64_t logits_ld, const float* labels,
