@@ -337,6 +337,7 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
         packs.append(PackedIndices(data.reshape(len(cols), Bg, L)))
     x = torch.randn((batch_local, D), device=device, generator=g).to(dt)
     dout = (torch.randn((batch_local, eng.width), device=device, generator=g) * 1e-3).to(dt)
+    eng.bench_packs = packs  # the index batches (tools/bench_full_step.py drives the full step with them)
 
     def step(k):
         if eng._graphs is not None:

@@ -3,6 +3,9 @@
 (whose `value` stays the hot path the BASELINE metric names).
 
     python tools/bench_full_step.py [--workload kaggle-d128-b2048] [--steps 48] [--warmup 8]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_full_step.py
+        (N ranks: ShardedDLRMModel = data-parallel MLPs with bucketed all-reduce + table-sharded hot
+         path, B samples per rank, eager launches; prints the whole-job samples/s)
 
 Model: kaggle_dlrm's MLPs (criteo.jl:408-433: bottom [13, 512, 256, D], top [D+P, 1024, 1024, 512,
 256, 1]) with GlorotNormal weights, the workload's tables (ScaledUniform), synthetic N(0,1) dense
@@ -49,6 +52,54 @@ def timed(g, reps):
     return (time.perf_counter() - t0) * 1e3 / (reps * NB)
 
 
+def main_sharded(a, pkg):
+    """One rank of the multi-GPU full step (SURVEY rows f1 + f3)."""
+    import torch.distributed as dist
+    from dlrm_jl_amd.sharded import make_bench_engine
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
+    backend = os.environ.get("DLRM_DIST_BACKEND", "nccl")  # "gloo": 1-GPU rehearsal only
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+    w = pkg.WORKLOADS[a.workload]
+    D, B, T = w["dim"], w["batch"], len(w["rows"])
+    eng, _, _ = make_bench_engine(pkg, w, B, dev, rank, world, a.lr)
+    gen = torch.Generator(device=dev).manual_seed(4242)  # identical MLP replicas on every rank
+    bsz, tsz = pkg.kaggle_mlp_sizes(D, T)
+    bottom = pkg.random_mlp(bsz, sigmoid_last=False, generator=gen, device=dev)
+    top = pkg.random_mlp(tsz, sigmoid_last=True, generator=gen, device=dev)
+    model = pkg.ShardedDLRMModel(bottom, top, eng, a.lr)
+    g2 = torch.Generator(device=dev).manual_seed(51234 + rank)
+    dense = [torch.randn((B, 13), device=dev, generator=g2) for _ in range(NB)]
+    labels = [(torch.rand((B,), device=dev, generator=g2) < 0.25).float() for _ in range(NB)]
+    for k in range(a.warmup):
+        model.step(dense[k % NB], eng.bench_packs[k % NB], labels[k % NB])
+    torch.cuda.synchronize()
+    eng.ops.ctx.check_bounds()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        loss = model.step(dense[k % NB], eng.bench_packs[k % NB], labels[k % NB])
+    torch.cuda.synchronize()
+    dist.barrier()
+    ms = torch.tensor([(time.perf_counter() - t0) * 1e3 / a.steps], device=dev)
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"DLRM full training step samples/s (MLPs + BCE + hot path + Descent), {world} MI355X",
+            "value": round(B * world / (float(ms) * 1e-3), 1), "unit": "samples/s", "ms_per_step": round(float(ms), 4),
+            "n_gpus": world, "scaling": "weak", "dtype": "f32", "loss_last": round(float(loss), 5),
+            "config": {"workload": a.workload, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"data-parallel MLPs (all-reduce) + table-sharded x{world} (all-to-all)",
+                       "launch": "eager", "backend": backend}}))
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="kaggle-d128-b2048")
@@ -57,6 +108,8 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     a = ap.parse_args()
     pkg = dlrm_pkg.load()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return main_sharded(a, pkg)
     dev = torch.device("cuda:0")
     w = pkg.WORKLOADS[a.workload]
     if w["lookups"] != 1 or w["dtype"] != "f32":
