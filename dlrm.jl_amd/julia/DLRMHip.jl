@@ -344,4 +344,47 @@ function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}) where {T}
     return Array(st.dx)
 end
 
+#####
+##### DACLoader replacement (src/data/criteo.jl:309-340): records uploaded raw, load! on the GPU
+#####
+
+"""
+    HipDACLoader(ctx, dataset::Vector{DACRecord}, batchsize)
+
+Iterates like `DACLoader` (whole batches only, `length = div(length(dataset), batchsize)`) and
+yields `(; labels, dense, sparse)` in HBM: `labels` 1 × B Float32, `dense` 13 × B Float32 and
+`sparse` a `PackedIndices` over the `Matrix{UInt32}(B, 26)` layout (1-based ids), ready for
+`maplookup` / `train_step_fwd!`.  `DACRecord` is bit-compatible with `dlrm_dac_record` (160 B),
+so each batch is one upload of the mmap'd records and one `dlrm_dac_decode` launch.
+"""
+struct HipDACLoader{V}
+    ctx::Context
+    dataset::V
+    batchsize::Int
+    raw::DeviceMatrix{UInt8}
+    labels::DeviceMatrix{Float32}
+    dense::DeviceMatrix{Float32}
+    sparse::DeviceMatrix{Int32}
+end
+function HipDACLoader(ctx::Context, dataset::AbstractVector, batchsize::Integer)
+    @assert sizeof(eltype(dataset)) == 160 "DACRecord is 160 bytes (criteo.jl:91-95)"
+    B = Int(batchsize)
+    return HipDACLoader(ctx, dataset, B, DeviceMatrix{UInt8}(ctx, 160, B), DeviceMatrix{Float32}(ctx, 1, B),
+                        DeviceMatrix{Float32}(ctx, 13, B), DeviceMatrix{Int32}(ctx, B, 26))
+end
+Base.length(l::HipDACLoader) = div(length(l.dataset), l.batchsize)
+function Base.iterate(l::HipDACLoader, i = 1)
+    i > length(l) && return nothing
+    B = l.batchsize
+    recs = view(l.dataset, (B * (i - 1) + 1):(B * i))
+    GC.@preserve recs begin
+        check(l.ctx, ccall((:dlrm_memcpy_h2d, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t),
+                           l.ctx.ptr, l.raw.ptr, pointer(recs), 160 * B))
+    end
+    check(l.ctx, ccall((:dlrm_dac_decode, libdlrm), Cint,
+                       (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Cint, Int64),
+                       l.ctx.ptr, l.raw.ptr, B, l.labels.ptr, l.dense.ptr, 13, l.sparse.ptr, DLRM_I32, B))
+    return (; labels = l.labels, dense = l.dense, sparse = PackedIndices(l.sparse, B, 1)), i + 1
+end
+
 end # module
