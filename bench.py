@@ -445,7 +445,9 @@ def main():
                      "indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)"),
             "config": {"workload": a.workload, "tables": T, "dim": D, "batch_per_gpu": B, "global_batch": B * world,
                        "lookups": L, "index_dtype": "int32", "table_rows": w.get("rows_src", "Criteo-Kaggle (criteo.jl:350-377)"),
-                       "parallelism": "single-gpu" if world == 1 else f"table-sharded x{world} + RCCL all-to-all",
+                       "parallelism": ("single-gpu" if world == 1 else f"table-sharded x{world} + "
+                                       + ("RCCL all-to-all" if dist.get_backend() == "nccl" else
+                                          f"{dist.get_backend()} all-to-all (host-staged rehearsal)")),
                        "launch": (f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else
                                   "hipGraph replay of the compute between eager all-to-alls" if a.mode == "segments"
                                   else "eager"),
