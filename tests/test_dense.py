@@ -326,3 +326,33 @@ def test_data_parallel_full_step_two_ranks_equals_single_gpu(pkg, gpu, tmp_path)
                 assert_close(z[f"{name}_b{i}"], m.b[i].cpu().numpy(), rtol=1e-5, what=f"rank {r} {name} b{i}")
         for t in part.tables(r):
             assert_close(z[f"t{t}"], model.tables[t].data.cpu().numpy(), rtol=1e-5, what=f"rank {r} table {t}")
+
+
+@pytest.mark.gpu
+def test_train_step_bf16_tables(pkg, gpu, golden, dense_golden):
+    """bf16 tables (SURVEY configs[2]'s storage) under the fp32 MLPs: the hot path computes in bf16
+    storage / fp32 accumulation, x and dLoss/dout cross the boundary rounded to bf16.  Loss and
+    updated rows agree with the fp32 golden step to bf16 precision."""
+    g, gd = golden["single"], dense_golden["single"]
+    T, N, D = g["emb"].shape
+    B = g["mlp_bottom"].shape[0]
+    lr = float(g["lr"])
+    tabs = [torch.from_numpy(t).to(gpu).to(torch.bfloat16) for t in g["emb"]]
+    start = [t.float().cpu().numpy() for t in tabs]
+    model = pkg.DLRMModel(_mlp(pkg, gd, "bot", False, gpu), tabs, _mlp(pkg, gd, "top", True, gpu), B, 1, lr=lr,
+                          index_base=0)
+    idx = pkg.PackedIndices(torch.from_numpy(g["idx"]).to(torch.int32).reshape(T, B, 1).to(gpu))
+    loss = float(model.step(torch.from_numpy(gd["input_bot"]).to(gpu), idx, torch.from_numpy(gd["labels"]).to(gpu)))
+    torch.cuda.synchronize()
+    model.hot.check_bounds()
+    assert abs(loss - float(gd["loss"])) <= 1e-2 * abs(float(gd["loss"]))
+    for t in range(T):
+        rows = g[f"upd_rows_{t}"]
+        got = model.tables[t].data.float().cpu().numpy()
+        want_delta = g[f"upd_vals_{t}"] - g["emb"][t][rows]  # the golden step's change of each touched row
+        got_delta = got[rows] - start[t][rows]
+        # bf16 storage: each row moves by the golden delta up to bf16 rounding of the row values
+        tol = 2 * 2.0 ** -8 * np.abs(start[t][rows]).max() + 0.05 * np.abs(want_delta).max()
+        assert np.abs(got_delta - want_delta).max() <= tol, t
+        untouched = np.setdiff1d(np.arange(N), rows)
+        assert np.array_equal(got[untouched], start[t][untouched])
