@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    ap.add_argument("--mode", choices=["auto", "graph", "eager"], default="auto",
+                    help="auto: hipGraph replay, except eager launches for pooled bags on one GPU (measured "
+                         "2.10M vs 2.00M samples/s: eager lets the side-stream indexer overlap the gather)")
     ap.add_argument("--overlap-indexer", type=int, default=-1, help="-1: the engine's default")
     ap.add_argument("--fused", type=int, default=1)
     ap.add_argument("--materialize-ys", type=int, default=-1,
@@ -205,6 +207,8 @@ def main():
             dist.init_process_group(backend)
     w = dict(pkg.WORKLOADS[a.workload])
     B, D, L = w["batch"], w["dim"], w["lookups"]
+    if a.mode == "auto":
+        a.mode = "eager" if (L > 1 and world == 1) else "graph"
     rows = w["rows"]
     T = len(rows)
     E = 4 if w["dtype"] == "f32" else 2
