@@ -6,8 +6,9 @@ One step = one training pass of the hot path over one batch (src/train/train.jl:
 the dense MLPs): maplookup -> DotInteraction -> dot_back -> update!(Descent) of the tables,
 with the dense vector x and dLoss/d(out) supplied as synthetic inputs already in HBM.
 Default workload (BASELINE metric): 26 Criteo-Kaggle tables (criteo.jl:350-377) x 128-dim
-fp32, 2048 samples per GPU, one-hot int32 indices drawn uniformly per table, 8 distinct
-batches cycled.  N > 1 (torchrun): tables sharded by table across ranks, per-GPU batch fixed
+fp32, 2048 samples per GPU, one-hot int32 indices drawn uniformly per table, 64 distinct
+batches cycled (their touched rows far exceed the 256 MiB Infinity Cache, so the timed gathers
+read HBM, not a warm MALL).  N > 1 (torchrun): tables sharded by table across ranks, per-GPU batch fixed
 (weak scaling), RCCL all-to-all of the looked-up vectors forward and of their gradients
 backward (dlrm.jl_amd/sharded.py).  Rank 0 prints ONE JSON line.
 """
@@ -27,7 +28,8 @@ import dlrm_pkg  # noqa: E402
 
 METRIC = "DLRM samples/sec (fwd+bwd), 26 tables×128-dim bs=2048; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
-NBATCH = 8
+NBATCH = 64  # distinct index batches cycled (--nbatch)
+CHUNK = 64  # steps per captured hipGraph
 
 
 def parse():
@@ -48,6 +50,9 @@ def parse():
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
                          "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
     ap.add_argument("--stage-timing", type=int, default=1, help="0: skip the per-stage telemetry (traces)")
+    ap.add_argument("--nbatch", type=int, default=NBATCH, help="distinct index batches cycled")
+    ap.add_argument("--sustain", type=float, default=2.0,
+                    help="seconds of back-to-back steps timed after the K-step region (reported as 'sustained')")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: build the next batch's indexer on a side stream during each step (step API only; "
                          "measured slower: 57.5 vs 49.6 us, the graph runs the side branch serially)")
@@ -107,7 +112,7 @@ def index_stats(idx_np):
     return {"n1": n1, "n2": n2, "u2": u2, "uniq": uniq}
 
 
-def make_inputs(pkg, w, B, dev, rank, T_rows):
+def make_inputs(pkg, w, B, dev, rank, T_rows, nbatch):
     """Tables ~ ScaledUniform (model.jl:61-65), x ~ N(0,1), dout ~ N(0, 1e-3)."""
     g = torch.Generator(device=dev).manual_seed(51234 + rank)  # model.jl:193 seed
     dt = torch.float32 if w["dtype"] == "f32" else torch.bfloat16
@@ -120,9 +125,10 @@ def make_inputs(pkg, w, B, dev, rank, T_rows):
     idx = []
     zipf = w.get("zipf")
     rng = np.random.default_rng(51234 + rank)
-    for _ in range(NBATCH):
+    perms = [pkg.zipf_perm(rng, n) for n in T_rows] if zipf else None  # the same rows stay hot
+    for _ in range(nbatch):
         if zipf:
-            cols = [torch.from_numpy(pkg.zipf_rows(rng, n, B * L, zipf)) for n in T_rows]
+            cols = [torch.from_numpy(pkg.zipf_rows(rng, n, B * L, zipf, p)) for n, p in zip(T_rows, perms)]
             idx.append(torch.stack(cols).to(dev).contiguous())
             continue
         cols = [torch.randint(0, n, (B * L,), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
@@ -136,6 +142,8 @@ def cpu_baseline(pkg, w, seconds, threads):
     tables in DRAM, same batch size.  Rank 0, N=1 only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    native = oracle.use_native()  # gcc -march=native on this host (falls back to the x86-64-v3 build)
+    model, host_cpus, allowed = oracle.host_cpu()
     rows = w["rows"]
     D, B, L = w["dim"], w["batch"], w["lookups"]
     T = len(rows)
@@ -172,9 +180,12 @@ def cpu_baseline(pkg, w, seconds, threads):
             break
     del tables
     return {"value": B * n / el, "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": host_cpus, "cpus_allowed": allowed,
+            "build": "gcc -O3 -march=native -fopenmp" if native else "gcc -O3 -march=x86-64-v3 -fopenmp",
             "sample": f"C/OpenMP restatement of the same step (oracle/dlrm_oracle.c), {T} tables x {D} "
                       f"fp32 in host DRAM ({sum(rows) * D * 4 / 1e9:.1f} GB), B={B}, {n} timed steps "
-                      f"({el:.1f} s) after 1 warm-up; not the Julia reference (no julia toolchain)"}
+                      f"({el:.1f} s) after 1 warm-up, {threads} OpenMP threads on {model}; not the Julia "
+                      f"reference (no julia toolchain)"}
 
 
 def load_pmc(workload, kernel):
@@ -212,9 +223,10 @@ def main():
     rows = w["rows"]
     T = len(rows)
     E = 4 if w["dtype"] == "f32" else 2
+    nb = a.nbatch
 
     if world == 1:
-        tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows)
+        tables, idx, g = make_inputs(pkg, w, B, dev, rank, rows, nb)
         ts = pkg.EmbeddingTableSet(tables)
         engine = pkg.HotPath(ts, B, L, lr=a.lr, index_base=0,
                              overlap_indexer=None if a.overlap_indexer < 0 else bool(a.overlap_indexer),
@@ -231,13 +243,13 @@ def main():
 
         if engine.pipeline:
             def step(k):
-                engine.step_next(x, packs[k % NBATCH], dout, packs[(k + 1) % NBATCH])
+                engine.step_next(x, packs[k % nb], dout, packs[(k + 1) % nb])
         else:
             def step(k):
-                engine.step(x, packs[k % NBATCH], dout)
+                engine.step(x, packs[k % nb], dout)
     else:
         from dlrm_jl_amd.sharded import make_bench_engine
-        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr)
+        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb)
         if a.mode == "graph":
             # the compute between the two all-to-alls is replayed as hipGraphs; the collectives
             # are launched eagerly (RCCL inside hipGraph capture: not relied on)
@@ -261,36 +273,50 @@ def main():
     elif engine.ops is not None:
         engine.ops.ctx.check_bounds()
 
-    # hipGraphs: one graph holds NBATCH consecutive steps (one per index batch), so the
-    # per-replay launch gap (~8 us measured on MI355X) is paid once per NBATCH steps; single-step
-    # graphs cover a remainder.  Within a graph the kernels run back to back.
-    graphs = None
-    multi = None
+    # hipGraphs: a graph holds up to CHUNK consecutive steps (one index batch each), so the
+    # per-replay launch gap (~8 us measured on MI355X) is paid once per graph, not per step.
+    # The timed K steps replay graphs of exactly the steps they stand for: full CHUNK-step graphs
+    # plus one graph of the remainder (captured once here, outside the timed region).
+    nb = a.nbatch
+    chunk = min(CHUNK, nb)
+    graphs = {}
     if world == 1 and engine.pipeline:
         engine.prime(packs[0])  # the captured steps start at batch 0
+
+    def capture(start, n):
+        cur = torch.cuda.current_stream()
+        s = torch.cuda.Stream()
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                for k in range(start, start + n):
+                    step(k)
+        cur.wait_stream(s)
+        gr.replay()
+        return gr
+
+    def plan(n):
+        """(start, length) pieces of steps [0, n): whole chunks cycling over the nb batches + a tail."""
+        out, k = [], 0
+        while n - k >= chunk:
+            out.append(((k % nb), chunk))
+            k += chunk
+        if n > k:
+            out.append(((k % nb), n - k))
+        return out
+
     if a.mode == "graph":
         try:
-            graphs = []
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for k in range(NBATCH):
-                    gr = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gr, stream=s):
-                        step(k)
-                    graphs.append(gr)
-                multi = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(multi, stream=s):
-                    for k in range(NBATCH):
-                        step(k)
-            torch.cuda.current_stream().wait_stream(s)
-            for k in range(NBATCH):
-                graphs[k].replay()
-            multi.replay()
+            for piece in set(plan(a.steps)) | set(plan(nb)):
+                if piece not in graphs:
+                    graphs[piece] = capture(*piece)
             torch.cuda.synchronize()
         except Exception as e:  # graph capture unsupported: eager
             print(f"note: graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
-            graphs = multi = None
+            graphs = None
+    else:
+        graphs = None
 
     def run_steps(n):
         """n consecutive steps starting at batch 0."""
@@ -298,25 +324,38 @@ def main():
             for k in range(n):
                 step(k)
             return
-        for _ in range(n // NBATCH):
-            multi.replay()
-        for k in range(n % NBATCH):
-            graphs[k].replay()
+        for piece in plan(n):
+            graphs[piece].replay()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_steps(a.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    ms = el * 1e3 / a.steps
-    if world > 1:
-        tt = torch.tensor([ms], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ms = float(tt.item())
+    def timed(n):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_steps(n)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ms = (time.perf_counter() - t0) * 1e3 / n
+        if world > 1:
+            tt = torch.tensor([ms], device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ms = float(tt.item())
+        return ms
+
+    ms = timed(a.steps)
+    # sustained: >= a.sustain seconds of back-to-back steps (whole cycles over the nb batches), so a
+    # short K does not hide clock ramp or cache effects; reported beside value, not instead of it
+    sustained = None
+    if a.sustain > 0:
+        cyc = max(1, int(np.ceil(a.sustain * 1e3 / (ms * nb))))
+        if world > 1:  # every rank runs the same number of steps
+            tc = torch.tensor([cyc], device=dev)
+            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+            cyc = int(tc.item())
+        ms_s = timed(cyc * nb)
+        sustained = {"steps": cyc * nb, "seconds": round(ms_s * cyc * nb / 1e3, 3), "ms_per_step": round(ms_s, 4),
+                     "value": round(B * world / (ms_s / 1e3), 1)}
     value = B * world / (ms / 1e3)
 
     # ---- per-kernel timing (HIP events on the launch stream) + roofline, rank 0
@@ -324,18 +363,18 @@ def main():
     stages = None
     if rank == 0 and world == 1 and a.stage_timing:
         uniq = chunks = 0
-        for k in range(NBATCH):
+        for k in range(nb):
             engine.build_indexer(packs[k])
             torch.cuda.synchronize()
             for t in range(T):
                 uniq += len(engine.indexer.unique_rows(t))
-        uniq /= NBATCH
+        uniq /= nb
         chunks = uniq  # one chunk per unique row, plus a few for hot rows
         bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks, engine.materialize_ys)
         # one prebuilt indexer per index batch, so the update stage can be timed on its own
-        indexers = [pkg.SparseIndexer(T, B * L, dev) for _ in range(NBATCH)]  # not the engine's own
+        indexers = [pkg.SparseIndexer(T, B * L, dev) for _ in range(nb)]  # not the engine's own
         home = engine.indexer
-        for k in range(NBATCH):
+        for k in range(nb):
             engine.indexer = indexers[k]
             engine.build_indexer(packs[k])
         engine.indexer = home
@@ -348,10 +387,10 @@ def main():
         in_bwd = (engine.fused and not engine.materialize_ys and engine.indexer is not None
                   and not engine.overlap_indexer)
         if engine.step_api:
-            sts = [index_stats(packs[k].data.reshape(T, B * L).cpu().numpy()) for k in range(NBATCH)]
-            st = {key: sum(v[key] for v in sts) / NBATCH for key in sts[0]}
+            sts = [index_stats(packs[k].data.reshape(T, B * L).cpu().numpy()) for k in range(nb)]
+            st = {key: sum(v[key] for v in sts) / nb for key in sts[0]}
             bytes_ = step_api_bytes(B, T, D, L, E, 4, st, pipelined=engine.pipeline)
-            for k in range(NBATCH):  # batch k's split indexer, built by its own step forward
+            for k in range(nb):  # batch k's split indexer, built by its own step forward
                 engine.indexer = indexers[k]
                 engine.step_fwd(x, packs[k])
             engine.indexer = home
@@ -388,11 +427,11 @@ def main():
             fns = [lambda k: engine.lookup(packs[k]), lambda k: engine.interact_fwd(x),
                    lambda k: engine.build_indexer(packs[k]), lambda k: engine.interact_bwd(dout, x=x, idx=packs[k]),
                    apply_k]
-        # Each stage: a hipGraph of its kernel(s) over the NBATCH index batches (the same batches the
+        # Each stage: a hipGraph of its kernel(s) over the nb index batches (the same batches the
         # timed loop cycles, so caches are no warmer than there), replayed REPS times between two HIP
-        # events on the launch stream; per-launch time = elapsed / (REPS * NBATCH).  Back-to-back
+        # events on the launch stream; per-launch time = elapsed / (REPS * nb).  Back-to-back
         # graph nodes carry no event markers, so this agrees with rocprofv3's per-kernel average.
-        reps = max(1, min(8, a.steps // NBATCH))
+        reps = max(2, min(8, a.steps // nb))
         stages = {}
         cur = torch.cuda.current_stream()
         for n, fn in zip(names, fns):
@@ -403,7 +442,7 @@ def main():
                 with torch.cuda.stream(s):
                     gr = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gr, stream=s):
-                        for k in range(NBATCH):
+                        for k in range(nb):
                             fn(k)
                 cur.wait_stream(s)
 
@@ -411,7 +450,7 @@ def main():
                 if gr is not None:
                     gr.replay()
                 else:
-                    for k in range(NBATCH):
+                    for k in range(nb):
                         fn(k)
 
             once()
@@ -421,7 +460,7 @@ def main():
                 once()
             e1.record(cur)
             torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / (reps * NBATCH)
+            us = e0.elapsed_time(e1) * 1e3 / (reps * nb)
             stages[n] = {"us": round(us, 2), "alg_bytes": int(bytes_[n]),
                          "GBps": round(bytes_[n] / (us * 1e-6) / 1e9, 1)}
         # the dominant kernel of the step's critical path (a side-stream stage overlaps it)
@@ -434,7 +473,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and w["dtype"] == "f32":
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        # every CPU this process may run on, capped by the OMP_NUM_THREADS share the host grants a
+        # one-GPU job (16 on the GPU box; its machine has more: host_cpus in the line)
+        allowed = len(os.sched_getaffinity(0))
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        threads = min(allowed, cap) if cap > 0 else allowed
         try:
             cpu = cpu_baseline(pkg, w, a.cpu_seconds, threads)
         except Exception as e:
@@ -452,7 +495,8 @@ def main():
                        "parallelism": ("single-gpu" if world == 1 else f"table-sharded x{world} + "
                                        + ("RCCL all-to-all" if dist.get_backend() == "nccl" else
                                           f"{dist.get_backend()} all-to-all (host-staged rehearsal)")),
-                       "launch": (f"hipGraph replay ({NBATCH} steps per graph)" if graphs is not None else
+                       "index_batches": nb,
+                       "launch": (f"hipGraph replay (<= {chunk} steps per graph)" if graphs is not None else
                                   "hipGraph replay of the compute between eager all-to-alls" if a.mode == "segments"
                                   else "eager"),
                        "ys": ("received blocks read in place (no ys)" if world > 1 else "materialized"
@@ -462,7 +506,7 @@ def main():
                                 if world == 1 and engine.pipeline else
                                 "dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "
                                 "updated in the backward)" if world == 1 and engine.step_api else "operators")},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "sustained": sustained, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     if world > 1:

@@ -15,7 +15,7 @@ from .embedding import (DefaultStrategy, EmbeddingTableSet, PackedIndices, Preal
 from .hotpath import HotPath
 from .interact import (POST_INTERACTION_PAD_TO_MUL, DotInteraction, cdiv, dot_back, fast_vcat, interaction_sizes,
                        rrule, up_to_mul_of)
-from .shapes import KAGGLE_EMBEDDING_SIZES, TERABYTE_EMBEDDING_SIZES, WORKLOADS, zipf_rows
+from .shapes import KAGGLE_EMBEDDING_SIZES, TERABYTE_EMBEDDING_SIZES, WORKLOADS, zipf_perm, zipf_rows
 from .update import Descent, SparseEmbeddingUpdate, SparseIndexer, maplookup_pullback, update_
 
 __all__ = [

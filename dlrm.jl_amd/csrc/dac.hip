@@ -114,6 +114,7 @@ extern "C" int dlrm_dac_parse_tsv(const char* text, int64_t len, dlrm_dac_record
             int64_t v;
             if (k == 0) {  // label: parse(Int32, ...; base = 10), never empty
                 if (f == fe_trim || !parse_int(f, fe_trim, 10, true, &v)) return DLRM_E_ARG;
+                if (v < INT32_MIN || v > INT32_MAX) return DLRM_E_ARG;  // parse(Int32, ...) throws OverflowError
                 r.label = (int32_t)v;
             } else if (k <= 13) {  // logtransform(emptyparse(Int32, ...; base = 10))
                 if (!parse_int(f, fe_trim, 10, true, &v) || v < INT32_MIN || v > INT32_MAX) return DLRM_E_ARG;
@@ -224,6 +225,7 @@ struct dlrm_dac_loader {
     std::mutex mu;
     std::condition_variable cv;
     bool slot_free[2] = {true, true};
+    bool held[2] = {false, false};  // handed to the caller by next, not yet released
     std::deque<int> ready_q;
     int64_t produced = 0, nbatches = 0;
     bool stop = false, running = false;
@@ -325,6 +327,12 @@ extern "C" int dlrm_dac_loader_create(int device, const dlrm_dac_record* records
 
 extern "C" int dlrm_dac_loader_start(dlrm_dac_loader* L, int64_t* nbatches) {
     if (!L) return DLRM_E_ARG;
+    {
+        // a slot the caller still holds may still be read on its stream: refilling it for a new
+        // epoch would overwrite a live batch (and a second live iterator would share ready_q)
+        std::lock_guard<std::mutex> g(L->mu);
+        if (L->held[0] || L->held[1]) return DLRM_E_STATE;
+    }
     dac_loader_join(L);  // a previous epoch's worker, if any
     // the previous epoch's uploads must have left the pinned buffers / raw slots
     if (L->stream && hipStreamSynchronize(L->stream) != hipSuccess) return DLRM_E_HIP;
@@ -353,6 +361,7 @@ extern "C" int dlrm_dac_loader_next(dlrm_dac_loader* L, void* consumer_stream, i
         }
         s = L->ready_q.front();
         L->ready_q.pop_front();
+        L->held[s] = true;
     }
     if (hipStreamWaitEvent((hipStream_t)consumer_stream, L->ready[s], 0) != hipSuccess) return DLRM_E_HIP;
     *slot = s;
@@ -364,6 +373,7 @@ extern "C" int dlrm_dac_loader_release(dlrm_dac_loader* L, int slot, void* consu
     if (hipEventRecord(L->consumed[slot], (hipStream_t)consumer_stream) != hipSuccess) return DLRM_E_HIP;
     std::lock_guard<std::mutex> g(L->mu);
     L->consumed_valid[slot] = true;
+    L->held[slot] = false;
     L->slot_free[slot] = true;
     L->cv.notify_all();
     return DLRM_OK;

@@ -193,6 +193,7 @@ class DACLoader:
         # straight out of it (no host memcpy, no host wait); else the pinned staging buffers
         self._registered = None
         self._nl = None
+        self._iterating = False
         nb = self._raw.nbytes
         if direct and 0 < nb <= DIRECT_MAX_BYTES and self._raw.flags.c_contiguous:
             addr = self._raw.ctypes.data
@@ -245,7 +246,11 @@ class DACLoader:
 
     def _iter_native(self, cur):
         lib = self.ctx.lib
+        if self._iterating:
+            raise RuntimeError("DACLoader: another iteration over this loader is still live (its batch "
+                               "buffers would be overwritten); finish or close it first")
         _lib.check(lib.dlrm_dac_loader_start(self._nl, None))
+        self._iterating = True
         st = ctypes.c_void_p(cur.cuda_stream)
         held = -1
         try:
@@ -262,6 +267,7 @@ class DACLoader:
             if held >= 0:
                 lib.dlrm_dac_loader_release(self._nl, held, st)
             lib.dlrm_dac_loader_stop(self._nl)
+            self._iterating = False
 
     def close(self):
         """Releases the page-locked dataset (after the queued copies have run) and the native loader."""

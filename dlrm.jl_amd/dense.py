@@ -227,9 +227,7 @@ class DLRMModel:
         """dlrm_bce_head on the top MLP's logits: prob, loss, dLoss/dlogit (self._dz) and the last
         layer's bias gradient, one launch."""
         B = z.shape[0]
-        if labels.shape != (B,) or labels.dtype != torch.float32 or not labels.is_contiguous():
-            raise ValueError(f"labels must be a contiguous float32 vector of {B}")
-        require_device(labels, z.device, "labels")
+        check_labels(labels, z)
         if self.prob is None or self.prob.shape[0] != B:
             self.prob = torch.empty(B, dtype=torch.float32, device=z.device)
             self.loss = torch.empty((), dtype=torch.float32, device=z.device)
@@ -253,6 +251,14 @@ class DLRMModel:
         self.top.sgd_(self.lr)
         self.bottom.sgd_(self.lr)
         return self.loss
+
+
+def check_labels(labels, z):
+    """dlrm_bce_head reads labels as a packed fp32 vector of the logits' batch on their device."""
+    B = z.shape[0]
+    if labels.shape != (B,) or labels.dtype != torch.float32 or not labels.is_contiguous():
+        raise ValueError(f"labels must be a contiguous float32 vector of {B}")
+    require_device(labels, z.device, "labels")
 
 
 def kaggle_mlp_sizes(feature_size, num_tables):
@@ -299,6 +305,7 @@ class ShardedDLRMModel:
         scale = 1.0 / self.world
         if z.is_cuda:
             B = z.shape[0]
+            check_labels(labels, z)
             if self.prob is None or self.prob.shape[0] != B:
                 self.prob = torch.empty(B, dtype=torch.float32, device=z.device)
                 self.loss = torch.empty((), dtype=torch.float32, device=z.device)
@@ -323,13 +330,14 @@ class ShardedDLRMModel:
         tables for the GLOBAL batch (ShardedHotPath's convention).  Returns the global-batch loss
         (a device scalar; the all-reduce is queued, not waited on by the host)."""
         x = self.bottom.forward(dense)
-        out = self.engine.forward(x.to(self.tdtype), idx)
+        xt = x.to(self.tdtype)  # the hot path reads x in the tables' dtype, forward and backward
+        out = self.engine.forward(xt, idx)
         z = self.top.forward(out.float(), logits=True)
         dz = self._head(z, labels)
         dout = self.top.backward(dz)
         multi = self.world > 1
         w_top = dist.all_reduce(self._top_flat, group=self.group, async_op=True) if multi else None
-        dx = self.engine.backward(idx, dout.to(self.tdtype).contiguous(), x)
+        dx = self.engine.backward(idx, dout.to(self.tdtype).contiguous(), xt)
         self.bottom.backward(dx, need_dx=False)
         if multi:
             dist.all_reduce(self._bot_flat, group=self.group)

@@ -43,12 +43,19 @@ def table_bytes(rows, dim, esize):
     return sum(rows) * dim * esize
 
 
-def zipf_rows(rng, n, size, s):
-    """Zipf(s) ranks (rank 0 hottest, tail folded mod n) scattered over the table's rows by an
-    affine bijection r -> (a*r + c) mod n, so hot rows sit at random places."""
-    z = (rng.zipf(s, size=size) - 1) % n
+def zipf_perm(rng, n):
+    """The affine bijection r -> (a*r + c) mod n that places a table's Zipf ranks on its rows.
+    Drawn once per table, so the same rows stay hot from batch to batch (hot-row skew)."""
     a = int(rng.integers(1, max(n, 2)))
     while np.gcd(a, n) != 1:
         a += 1
-    c = int(rng.integers(0, n))
+    return a, int(rng.integers(0, n))
+
+
+def zipf_rows(rng, n, size, s, perm=None):
+    """Zipf(s) ranks (rank 0 hottest, tail folded mod n) scattered over the table's rows by an
+    affine bijection r -> (a*r + c) mod n, so hot rows sit at random places.
+    perm: the table's (a, c) from zipf_perm (fixed across batches); None draws a fresh one."""
+    z = (rng.zipf(s, size=size) - 1) % n
+    a, c = zipf_perm(rng, n) if perm is None else perm
     return ((z.astype(np.int64) * a + c) % n).astype(np.int32)

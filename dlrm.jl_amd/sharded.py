@@ -36,7 +36,7 @@ from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices
 from .interact import interaction_sizes
 from .runtime import context, dtype_code, ptr
-from .shapes import zipf_rows
+from .shapes import zipf_perm, zipf_rows
 from .update import SparseIndexer
 
 
@@ -76,6 +76,9 @@ class TablePartition:
             r = min(range(world), key=lambda r: (load[r], len(owners[r])))
             owners[r].append(t)
             load[r] += rows[t]
+        if max(load) * row_bytes > capacity:
+            raise ValueError(f"no table partition over {world} ranks fits {capacity} bytes per rank: the greedy "
+                             f"assignment needs {[l * row_bytes for l in load]} bytes per rank")
         return cls(len(rows), world, [sorted(o) for o in owners])
 
     def tables(self, r):
@@ -302,8 +305,8 @@ class ShardedHotPath:
         upd[k].replay()
 
 
-def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None):
-    """Bench setup for one rank: local tables (full size) and NBATCH index batches for the
+def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None, nbatch=8):
+    """Bench setup for one rank: local tables (full size) and nbatch index batches for the
     global batch; returns (engine, step(k) closure, prepare_graphs() closure)."""
     import numpy as np
     rows = w["rows"]
@@ -323,13 +326,14 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
     Bg = batch_local * world
     ops = HipShardOps(tables, Bg, L, lr, device=device)
     eng = ShardedHotPath(ops, part, rank, batch_local, D, L, dt, device)
-    nb = 8
+    nb = nbatch
     packs = []
     zipf = w.get("zipf")
     rng = np.random.default_rng(seed + rank)
+    perms = {t: zipf_perm(rng, rows[t]) for t in mine} if zipf else None  # the same rows stay hot
     for _ in range(nb):
         if zipf:
-            cols = [torch.from_numpy(zipf_rows(rng, rows[t], Bg * L, zipf)).to(device) for t in mine]
+            cols = [torch.from_numpy(zipf_rows(rng, rows[t], Bg * L, zipf, perms[t])).to(device) for t in mine]
         else:
             cols = [torch.randint(0, rows[t], (Bg * L,), device=device, generator=g,
                                   dtype=torch.int64).to(torch.int32) for t in mine]

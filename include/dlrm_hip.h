@@ -297,8 +297,9 @@ int dlrm_dac_decode(dlrm_ctx* ctx, const dlrm_dac_record* records, int batch, fl
  * native worker thread (pinned staging, upload + dlrm_dac_decode on the loader's own stream).
  * next: blocks until the next batch is decoded, makes consumer_stream wait for it, returns its
  * slot (-1: epoch over).  release: the caller's work on that slot is queued on consumer_stream;
- * the slot may be refilled after it.  stop: ends the epoch early.  The calls for one loader
- * come from one host thread. */
+ * the slot may be refilled after it.  stop: ends the epoch early.  start returns DLRM_E_STATE
+ * while a slot of the previous epoch is still held (next without release).  The calls for one
+ * loader come from one host thread. */
 typedef struct dlrm_dac_loader dlrm_dac_loader;
 int dlrm_dac_loader_create(int device, const dlrm_dac_record* records, int64_t count, int batch, int itype,
                            float* const* labels, float* const* dense, void* const* sparse, dlrm_dac_loader** out);

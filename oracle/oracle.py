@@ -27,6 +27,37 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def use_native():
+    """Selects the -march=native build of the oracle, compiled by gcc on the host that calls this
+    (bench.py's cpu_baseline leg only).  Returns the path, or None (portable build kept)."""
+    global _LIB_PATH, _lib
+    path = os.path.join(_HERE, "build", "libdlrm_oracle_native.so")
+    if _lib is not None and _LIB_PATH == path:
+        return path
+    try:
+        if os.path.exists(path):
+            os.unlink(path)  # never reuse one built for another host's CPU
+        subprocess.check_call(["make", "-s", "-C", _HERE, "native"], timeout=120)
+    except Exception:
+        return None
+    _LIB_PATH, _lib = path, None
+    return path
+
+
+def host_cpu():
+    """(model name, logical CPUs of the machine, CPUs this process may run on)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1, len(os.sched_getaffinity(0))
+
+
 def lib():
     global _lib
     if _lib is None:

@@ -92,6 +92,11 @@ def test_parse_errors_and_unknown_values(pkg):
     line = open(ALLDAYS, "rb").readline()
     with pytest.raises(pkg.DLRMError):
         dac.parse_tsv(line.replace(b"\t", b"\tzz", 1))  # not a base-10 integer
+    label = line.split(b"\t", 1)
+    for big in (b"4294967295", b"2147483648", b"-2147483649"):  # parse(Int32, ...) throws OverflowError
+        with pytest.raises(pkg.DLRMError):
+            dac.parse_tsv(big + b"\t" + label[1])
+    assert dac.parse_tsv(b"-2147483648\t" + label[1])["label"][0] == -2147483648
     recs = dac.parse_tsv(line + line)
     assert len(recs) == 2 and np.array_equal(recs[0], recs[1])
     maps = dac.reindex(recs)
@@ -125,6 +130,9 @@ def test_dac_loader_batches_match_load(pkg, gpu, reindexed, itype, direct, nativ
         pass
     it = iter(loader)
     next(it)
+    if native:  # a live iteration holds a batch buffer: a second one must not start over it
+        with pytest.raises(RuntimeError):
+            next(iter(loader))
     it.close()
     assert len(loader) == 250 // 64  # whole batches only (criteo.jl:326-329)
     seen = 0

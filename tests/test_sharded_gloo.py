@@ -166,6 +166,8 @@ def test_partition_fits_terabyte_tables():
     assert max(p2.bytes_per_rank(rows, rb)) < 240e9
     with pytest.raises(ValueError):
         TablePartition(3, 2, [[0, 1], [1, 2]])
+    with pytest.raises(ValueError, match="bytes per rank"):  # 452 GB fp32 cannot fit one 288 GB GPU
+        TablePartition.fitting(rows, 1, rb, cap)
 
 
 # ---- the full training step, data-parallel MLPs + sharded tables (SURVEY §8 rows f1 + f3) ------

@@ -93,7 +93,7 @@ def main_sharded(a, pkg):
         print(json.dumps({
             "metric": f"DLRM full training step samples/s (MLPs + BCE + hot path + Descent), {world} MI355X",
             "value": round(B * world / (float(ms) * 1e-3), 1), "unit": "samples/s", "ms_per_step": round(float(ms), 4),
-            "n_gpus": world, "scaling": "weak", "dtype": "f32", "loss_last": round(float(loss), 5),
+            "n_gpus": world, "scaling": "weak", "dtype": w["dtype"] + " tables, f32 MLPs", "loss_last": round(float(loss), 5),
             "config": {"workload": a.workload, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"data-parallel MLPs (all-reduce) + table-sharded x{world} (all-to-all)",
                        "launch": "eager", "backend": backend}}))

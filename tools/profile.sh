@@ -11,7 +11,7 @@ TAG=${1:?tag}; WL=${2:?workload}; shift 2
 export TMPDIR=/tmp
 O=gpurun_out/prof_${TAG}_${WL}
 rm -rf "$O"; mkdir -p "$O"
-B="--workload $WL --steps 40 --warmup 5 --no-cpu-baseline $*"
+B="--workload $WL --steps 40 --warmup 5 --no-cpu-baseline --sustain 0 $*"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/kt" -o run --output-format csv -- python3 bench.py $B > "$O/kt.log" 2>&1 || { echo "kt pass failed"; tail -n 20 "$O/kt.log"; exit 1; }
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run --output-format csv -- python3 bench.py $B > "$O/fetch.log" 2>&1 || { echo "fetch pass failed"; tail -n 20 "$O/fetch.log"; exit 1; }
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o run --output-format csv -- python3 bench.py $B > "$O/write.log" 2>&1 || { echo "write pass failed"; tail -n 20 "$O/write.log"; exit 1; }
