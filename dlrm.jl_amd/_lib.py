@@ -21,6 +21,7 @@ F32, BF16 = 0, 1
 I32, I64 = 0, 1
 UPDATE_ATOMIC, UPDATE_PREBUILT = 1, 2
 STEP_BWD_ONLY, STEP_APPLY_ONLY = 1, 2
+COMM_ID_BYTES = 128
 
 
 class DLRMError(RuntimeError):
@@ -71,6 +72,10 @@ SIGNATURES = {
     "dlrm_interact_bwd": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp, _i64]),
     "dlrm_interact_bwd_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _i32,
                                         _vp, _i64, _vp, _i64]),
+    "dlrm_triangular_slice": (_i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64]),
+    "dlrm_triangular_slice_back": (_i32, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
+    "dlrm_self_batched_mul": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64]),
+    "dlrm_self_batched_mul_back": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64]),
     "dlrm_indexer_create": (_i32, [_vp, _i32, _i64, _pp]),
     "dlrm_indexer_destroy": (_i32, [_vp]),
     "dlrm_indexer_build": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32]),
@@ -93,6 +98,11 @@ SIGNATURES = {
     "dlrm_dac_loader_release": (_i32, [_vp, _i32, _vp]),
     "dlrm_dac_loader_stop": (_i32, [_vp]),
     "dlrm_dac_loader_destroy": (_i32, [_vp]),
+    "dlrm_comm_unique_id": (_i32, [_vp]),
+    "dlrm_comm_init": (_i32, [_vp, _vp, _i32, _i32, _pp]),
+    "dlrm_comm_destroy": (_i32, [_vp]),
+    "dlrm_alltoall_fwd": (_i32, [_vp, _vp, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
+    "dlrm_alltoall_bwd": (_i32, [_vp, _vp, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),

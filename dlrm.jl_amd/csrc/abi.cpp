@@ -401,6 +401,56 @@ int dlrm_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int num_features, int bat
     return launch_interact_bwd(ctx, dtype, d, num_features, batch, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld);
 }
 
+// ---- Implementation 2 pieces (interact.jl:176-215, :503-551)
+int dlrm_triangular_slice(dlrm_ctx* ctx, int dtype, int sz, int batch, const void* z, int64_t z_batch_stride,
+                          void* out, int64_t out_ld) {
+    CHECK_ARG(ctx, "dlrm_triangular_slice: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_triangular_slice: dtype %d", dtype);
+    CHECK_ARG(sz >= 1 && batch >= 0, "dlrm_triangular_slice: sz=%d batch=%d", sz, batch);
+    CHECK_ARG(z_batch_stride >= (int64_t)sz * sz && out_ld >= (int64_t)sz * (sz - 1) / 2,
+              "dlrm_triangular_slice: strides too small");
+    CHECK_ARG(batch == 0 || sz < 2 || (z && out), "dlrm_triangular_slice: null buffer");  // sz = 1: no pairs
+    return launch_triangular_slice(ctx, dtype, sz, batch, z, z_batch_stride, out, out_ld);
+}
+
+int dlrm_triangular_slice_back(dlrm_ctx* ctx, int dtype, int sz, int batch, const void* dy, int64_t dy_ld, void* a,
+                               int64_t a_batch_stride, int symmetric) {
+    CHECK_ARG(ctx, "dlrm_triangular_slice_back: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_triangular_slice_back: dtype %d", dtype);
+    CHECK_ARG(sz >= 1 && batch >= 0, "dlrm_triangular_slice_back: sz=%d batch=%d", sz, batch);
+    CHECK_ARG(a_batch_stride >= (int64_t)sz * sz && dy_ld >= (int64_t)sz * (sz - 1) / 2,
+              "dlrm_triangular_slice_back: strides too small");
+    CHECK_ARG(batch == 0 || (a && (sz < 2 || dy)), "dlrm_triangular_slice_back: null buffer");
+    return launch_triangular_slice_back(ctx, dtype, sz, batch, dy, dy_ld, a, a_batch_stride, symmetric ? 1 : 0);
+}
+
+int dlrm_self_batched_mul(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* t, int64_t t_ld,
+                          void* z, int64_t z_batch_stride) {
+    CHECK_ARG(ctx, "dlrm_self_batched_mul: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_self_batched_mul: dtype %d", dtype);
+    CHECK_ARG(d > 0 && num_features >= 1 && batch >= 0, "dlrm_self_batched_mul: d=%d F=%d B=%d", d, num_features, batch);
+    if (num_features > 90) return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_self_batched_mul: F=%d > 90", num_features);
+    CHECK_ARG(t_ld >= (int64_t)num_features * d && z_batch_stride >= (int64_t)num_features * num_features,
+              "dlrm_self_batched_mul: strides too small");
+    CHECK_ARG(batch == 0 || (t && z), "dlrm_self_batched_mul: null buffer");
+    return launch_self_batched_mul(ctx, dtype, d, num_features, batch, t, t_ld, z, z_batch_stride);
+}
+
+int dlrm_self_batched_mul_back(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* t,
+                               int64_t t_ld, const void* dz, int64_t dz_batch_stride, float* dt, int64_t dt_ld) {
+    CHECK_ARG(ctx, "dlrm_self_batched_mul_back: null ctx");
+    CHECK_ARG(dtype == DLRM_F32 || dtype == DLRM_BF16, "dlrm_self_batched_mul_back: dtype %d", dtype);
+    CHECK_ARG(d > 0 && num_features >= 1 && batch >= 0, "dlrm_self_batched_mul_back: d=%d F=%d B=%d", d, num_features,
+              batch);
+    if (num_features > 90)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_self_batched_mul_back: F=%d > 90", num_features);
+    CHECK_ARG(t_ld >= (int64_t)num_features * d && dz_batch_stride >= (int64_t)num_features * num_features &&
+                  dt_ld >= (int64_t)num_features * d,
+              "dlrm_self_batched_mul_back: strides too small");
+    CHECK_ARG(batch == 0 || (t && dz && dt), "dlrm_self_batched_mul_back: null buffer");
+    return launch_self_batched_mul_back(ctx, dtype, d, num_features, batch, t, t_ld, dz, dz_batch_stride, dt, dt_ld);
+}
+
 int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
                              int64_t table_stride, int index_base, int batch, int lookups, const void* x,
                              int64_t x_ld, const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld,

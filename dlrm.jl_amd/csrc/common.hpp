@@ -250,6 +250,14 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
                      float lr);
+int launch_triangular_slice(dlrm_ctx* ctx, int dtype, int sz, int B, const void* z, int64_t z_bs, void* out,
+                            int64_t out_ld);
+int launch_triangular_slice_back(dlrm_ctx* ctx, int dtype, int sz, int B, const void* dy, int64_t dy_ld, void* a,
+                                 int64_t a_bs, int sym);
+int launch_self_batched_mul(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* t, int64_t t_ld, void* z,
+                            int64_t z_bs);
+int launch_self_batched_mul_back(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* t, int64_t t_ld,
+                                 const void* dz, int64_t dz_bs, float* dt, int64_t dt_ld);
 int launch_sgd_atomic(dlrm_ctx* ctx, TableDesc* tabs, int T, int D, const void* idx, int itype, int64_t tstride,
                       int base, int B, int L, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
                       float lr);

@@ -336,6 +336,7 @@ struct StepUpdate {
     const uint8_t* single;  // [T][cap]
     int64_t cap;
     float lr;
+    const unsigned* err;    // the ctx's bounds flag: set -> no table row is written (the row goes to dt)
 };
 
 template <typename T, int NB, bool GATHER, bool UPD = false, int SBU_ = 0, int DC = 0>
@@ -391,6 +392,9 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
         }
         uint32_t urow[NB][4];  // UPD: the once-hit table row of output row f = 16I + 4q + r, else ~0u
         if (UPD) {
+            // a bounds error of this step (raised by the forward): the reference's gather throws
+            // before update!, so every row goes to dt and the apply (which checks too) writes none
+            const bool frozen = *su.err != 0;
             uint8_t fl[NB][4];
             int64_t ui[NB][4];
 #pragma unroll
@@ -410,7 +414,7 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
                     const bool tab = f >= 1 && f < F;
                     const TableDesc td = tds[tab ? f - 1 : 0];
                     const int64_t rr = ui[I][r] - ga.base;
-                    urow[I][r] = (tab & (fl[I][r] != 0) & (rr >= 0) & (rr < td.nrows)) ? (uint32_t)rr : ~0u;
+                    urow[I][r] = (tab & !frozen & (fl[I][r] != 0) & (rr >= 0) & (rr < td.nrows)) ? (uint32_t)rr : ~0u;
                 }
         }
         // The first super-blocks' T rows (and dout's x part) go out before S is built, so their
@@ -898,7 +902,7 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
-    StepUpdate su{ix.single, ix.cap, lr};
+    StepUpdate su{ix.single, ix.cap, lr, ctx_error_word(ctx)};
     // one super-block of T rows in flight: two (the gather backward's choice) spill here
     static const int sbu = getenv("DLRM_UPD_SBU") ? atoi(getenv("DLRM_UPD_SBU")) : 1;  // experiment knob
 #define DLRM_LAUNCH_BWDUP(TY, N_)                                                                                  \

@@ -452,7 +452,11 @@ __device__ __forceinline__ void sgd_row4(TT* row, int c0, const f32x4& sum, floa
 template <typename TT, typename GT, int VPR, int CPG>
 __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_, int L,
                                                         const GT* __restrict__ grad, int64_t grad_ld,
-                                                        int64_t grad_offset, float lr) {
+                                                        int64_t grad_offset, float lr,
+                                                        const unsigned* __restrict__ err) {
+    // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
+    // this step): the reference's gather throws before update!, so no table row is written
+    if (*err) return;
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE;
     constexpr int D = G::D;
@@ -560,7 +564,8 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
 template <typename TT, typename GT>
 __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,
                                                          const GT* __restrict__ grad, int64_t grad_ld,
-                                                         int64_t grad_offset, float lr) {
+                                                         int64_t grad_offset, float lr, const unsigned* __restrict__ err) {
+    if (*err) return;
     const int t = blockIdx.y;
     const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
     const int64_t off = (int64_t)t * ix.cap;
@@ -580,7 +585,8 @@ __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDes
 template <typename TT, typename GT>
 __global__ __launch_bounds__(256) void sgd_hot_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,
                                                       const GT* __restrict__ grad, int64_t grad_ld,
-                                                      int64_t grad_offset, float lr) {
+                                                      int64_t grad_offset, float lr, const unsigned* __restrict__ err) {
+    if (*err) return;
     const int t = blockIdx.y;
     const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
     const int64_t off = (int64_t)t * ix.cap;
@@ -604,6 +610,7 @@ __global__ __launch_bounds__(256) void sgd_atomic_kernel(TableDesc* __restrict__
                                                          int base, int B, int L, const GT* __restrict__ grad,
                                                          int64_t grad_ld, int64_t grad_offset, float lr,
                                                          unsigned* __restrict__ err) {
+    if (*err) return;  // raised by validate_indices_kernel (launched first) or an earlier launch
     const int64_t N = (int64_t)B * L;
     const int64_t total = (int64_t)ntab * N * D;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -612,13 +619,26 @@ __global__ __launch_bounds__(256) void sgd_atomic_kernel(TableDesc* __restrict__
         const int t = (int)(item / N);
         const int64_t p = item - (int64_t)t * N;
         const int64_t r = load_index(idx, itype, t * tstride + p) - base;
-        if (r < 0 || r >= tabs[t].nrows) {
-            if (c == 0) raise_index_error(err);
-            continue;
-        }
+        if (r < 0 || r >= tabs[t].nrows) continue;  // (cannot happen: validated before the launch)
         const float gval = to_f32(grad[(p / L) * grad_ld + grad_offset + (int64_t)t * D + c]);
         unsafeAtomicAdd((float*)tabs[t].data + r * D + c, -lr * gval);
     }
+}
+
+// Bounds check of every index before the atomic update (which must not write a row when any
+// index of the step is out of range).
+__global__ __launch_bounds__(256) void validate_indices_kernel(const TableDesc* __restrict__ tabs, int ntab,
+                                                               const void* __restrict__ idx, int itype,
+                                                               int64_t tstride, int base, int64_t N,
+                                                               unsigned* __restrict__ err) {
+    const int64_t total = (int64_t)ntab * N;
+    bool bad = false;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(e / N);
+        const int64_t r = load_index(idx, itype, t * tstride + (e - (int64_t)t * N)) - base;
+        bad |= r < 0 || r >= tabs[t].nrows;
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) raise_index_error(err);
 }
 
 // ------------------------------------------------------------------------ launchers
@@ -665,7 +685,7 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
 
 template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
-                             int64_t grad_ld, int64_t grad_offset, float lr, int64_t N) {
+                             int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int CPG = 1;                   // chunks per lane group (4 measured slower)
     const int per_block = 4 * G::RPW * CPG;  // 4 waves x RPW lane groups x CPG chunks
@@ -684,14 +704,15 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     int64_t grid = (int64_t)per_cu * (cus > 0 ? cus : 256);
     if (grid > cb + hb) grid = cb + hb;
     hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, CPG>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(256), 0, s,
-                       ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr);
+                       ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err);
 }
 
 template <typename TT, typename GT>
 static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L,
-                           const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, int64_t N) {
+                           const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, int64_t N,
+                           const unsigned* err) {
 #define DLRM_CASE(V) \
-    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N); return true;
+    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err); return true;
     switch (vpr) {
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64) DLRM_CASE(128)
         default: return false;
@@ -705,6 +726,7 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     if (T_ == 0 || N == 0) return DLRM_OK;
     T_ <<= ix.vshift;  // virtual tables (row-parity halves) of a forward-launch build
     hipStream_t s = ctx_stream(ctx);
+    const unsigned* err = ctx_error_word(ctx);
     const int gesz = gdtype == DLRM_F32 ? 4 : 2;
     const int tesz = tdtype == DLRM_F32 ? 4 : 2;
     const bool aligned = tabs_aligned16 && (uintptr_t)grad % 16 == 0 && (grad_ld * gesz) % 16 == 0 &&
@@ -714,13 +736,13 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     if (aligned && slots < (1ll << 31)) {
         const int vpr = D * gesz / 16;
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
-            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N);
+            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
         else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32)
-            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N);
+            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
         else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16)
-            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N);
+            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
         else
-            done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N);
+            done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
     }
     if (!done) {
         const int64_t gx0 = (N * D + 255) / 256;
@@ -729,9 +751,9 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
         const unsigned hx = (unsigned)(hx0 < 1 ? 1 : (hx0 > 1024 ? 1024 : hx0));
 #define DLRM_SCALAR(TT, GT)                                                                                         \
     hipLaunchKernelGGL((sgd_chunks_scalar<TT, GT>), dim3(gx, T_), dim3(256), 0, s, ix, tabs, D, L, (const GT*)grad, \
-                       grad_ld, grad_offset, lr);                                                                   \
+                       grad_ld, grad_offset, lr, err);                                                              \
     hipLaunchKernelGGL((sgd_hot_scalar<TT, GT>), dim3(hx, T_), dim3(256), 0, s, ix, tabs, D, L, (const GT*)grad,    \
-                       grad_ld, grad_offset, lr);
+                       grad_ld, grad_offset, lr, err);
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32) { DLRM_SCALAR(float, float) }
         else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32) { DLRM_SCALAR(uint16_t, float) }
         else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16) { DLRM_SCALAR(float, uint16_t) }
@@ -746,9 +768,15 @@ int launch_sgd_atomic(dlrm_ctx* ctx, TableDesc* tabs, int T_, int D, const void*
                       float lr) {
     if (T_ == 0 || B == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
+    const int64_t cap = (int64_t)ctx_num_cus(ctx) * 16;
+    {
+        int64_t gv = ((int64_t)T_ * B * L + 255) / 256;
+        if (gv > cap) gv = cap;
+        hipLaunchKernelGGL(validate_indices_kernel, dim3((unsigned)gv), dim3(256), 0, s, tabs, T_, idx, itype, tstride,
+                           base, (int64_t)B * L, ctx_error_word(ctx));
+    }
     const int64_t total = (int64_t)T_ * B * L * D;
     int64_t g = (total + 255) / 256;
-    const int64_t cap = (int64_t)ctx_num_cus(ctx) * 16;
     if (g > cap) g = cap;
     if (gdtype == DLRM_F32)
         hipLaunchKernelGGL(sgd_atomic_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, tabs, T_, D, idx, itype, tstride,

@@ -101,6 +101,94 @@ def rrule(dot, x, ys):
     return forward, dot_pullback
 
 
+# ---- Implementation 2 (interact.jl:176-215, :503-554): the same interaction as separate operators
+def _check_3d(name, a, B, n, m):
+    if a.dim() != 3 or a.shape != (B, n, m) or a.stride(2) != 1 or a.stride(1) != m:
+        raise ValueError(f"{name} must be a [{B}][{n}][{m}] tensor with contiguous matrices")
+
+
+def triangular_slice(z):
+    """triangular_slice(X) (interact.jl:176-191) of a batch of square matrices.  z: [B][sz][sz]
+    (row-major view of Julia's (sz, sz, B): z[b][col][row] = X[row, col, b]) -> [B][sz(sz-1)/2],
+    entries with row < col in triangular_slice_kernel! order (:64-75).  Bit-exact copy."""
+    B, sz = z.shape[0], z.shape[1]
+    _check_3d("z", z, B, sz, sz)
+    out = torch.empty((B, sz * (sz - 1) // 2), dtype=z.dtype, device=z.device)
+    ctx = context(z.device)
+    ctx.check(ctx.lib.dlrm_triangular_slice(ctx.bind(), dtype_code(z.dtype), sz, B, ptr(z), z.stride(0), ptr(out),
+                                            out.stride(0)))
+    return out
+
+
+def triangular_slice_back(delta, sz, *, symmetric=False):
+    """triangular_slice_back(Δ, size) (interact.jl:193-203): [B][ncols] -> [B][sz][sz] with Δ on the
+    upper triangle (z[b][col][row], row < col) and zeros elsewhere (triangular_slice_back_kernel!,
+    :104-120); symmetric=True is the fused add-transpose form (:150-171)."""
+    B = delta.shape[0]
+    if delta.dim() != 2 or delta.shape[1] < sz * (sz - 1) // 2 or delta.stride(1) != 1:
+        raise ValueError("triangular_slice_back: Δ must be [B][>= sz(sz-1)/2] with contiguous rows")
+    a = torch.empty((B, sz, sz), dtype=delta.dtype, device=delta.device)
+    ctx = context(delta.device)
+    ctx.check(ctx.lib.dlrm_triangular_slice_back(ctx.bind(), dtype_code(delta.dtype), sz, B, ptr(delta),
+                                                 delta.stride(0), ptr(a), a.stride(0), 1 if symmetric else 0))
+    return a
+
+
+def rrule_triangular_slice(z):
+    """ChainRulesCore.rrule(triangular_slice, x) (interact.jl:205-215)."""
+    sz = z.shape[1]
+
+    def triangular_slice_pullback(delta):
+        return None, triangular_slice_back(delta, sz)
+
+    return triangular_slice(z), triangular_slice_pullback
+
+
+def self_batched_mul(t):
+    """self_batched_mul(T) (interact.jl:526-537): Z_b = T_bᵀ T_b over the feature dim.
+    t: [B][F][d] (Julia's (d, F, B)) -> [B][F][F] in t's dtype (fp32 accumulation)."""
+    B, F, d = t.shape
+    _check_3d("t", t, B, F, d)
+    z = torch.empty((B, F, F), dtype=t.dtype, device=t.device)
+    ctx = context(t.device)
+    ctx.check(ctx.lib.dlrm_self_batched_mul(ctx.bind(), dtype_code(t.dtype), d, F, B, ptr(t), t.stride(0), ptr(z),
+                                            z.stride(0)))
+    return z
+
+
+def rrule_self_batched_mul(t):
+    """ChainRulesCore.rrule(self_batched_mul, x) (interact.jl:539-551): dT = T (Δ + Δᵀ), fp32."""
+    B, F, d = t.shape
+    z = self_batched_mul(t)
+
+    def self_batched_mul_back(delta):
+        _check_3d("Δ", delta, B, F, F)
+        if delta.dtype != t.dtype:
+            raise TypeError("self_batched_mul_back: Δ and T must share a dtype")
+        dt = torch.empty((B, F, d), dtype=torch.float32, device=t.device)
+        ctx = context(t.device)
+        ctx.check(ctx.lib.dlrm_self_batched_mul_back(ctx.bind(), dtype_code(t.dtype), d, F, B, ptr(t), t.stride(0),
+                                                     ptr(delta), delta.stride(0), ptr(dt), dt.stride(0)))
+        return None, dt
+
+    return z, self_batched_mul_back
+
+
+def dot_interaction(x, ys):
+    """dot_interaction(X, Ys) (interact.jl:503-517), Implementation 2: fast_vcat, the full batched
+    Gram, its triangle, concat with X.  x: [B][d]; ys: [B][d + D*T] (rows 0:d reserved for x, as
+    maplookup(PreallocationStrategy(d)) leaves them) -> [B][d + F(F-1)/2].  One MFMA launch: the
+    composition is DotInteraction's forward with no padding (the same values)."""
+    return DotInteraction(pad_to=1)(x, ys)
+
+
+def rrule_dot_interaction(x, ys):
+    """Zygote's pullback of dot_interaction: through concat, triangular_slice's rrule (upper
+    triangle), self_batched_mul's (Δ + Δᵀ) and fast_vcat's -- dT = T S with S the symmetric
+    zero-diagonal unpack of Δ's pair rows, dx = Δ_x + dT's x rows: dot_back's math, one launch."""
+    return rrule(DotInteraction(pad_to=1), x, ys)
+
+
 def fast_vcat(x, ys):
     """fast_vcat(x, ys) (interact.jl:271-281): copy x into the top rows reserved in ys.
     DotInteraction already fuses this copy into its kernel; this standalone form exists for

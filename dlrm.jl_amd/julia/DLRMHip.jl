@@ -22,7 +22,8 @@ module DLRMHip
 
 using ChainRulesCore
 import EmbeddingTables
-import EmbeddingTables: maplookup, PreallocationStrategy, SparseEmbeddingUpdate, Static
+import EmbeddingTables: maplookup, DefaultStrategy, PreallocationStrategy, SparseEmbeddingUpdate, Static
+import OneDNN   # the bottom MLP's output / the top MLP's cotangent arrive as OneDNN.Memory
 
 const libdlrm = joinpath(@__DIR__, "..", "lib", "libdlrm_hip.so")
 
@@ -164,10 +165,15 @@ end
 ##### maplookup (src/model/model.jl:161) + its pullback
 #####
 
-function _maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse) where {D,T}
+# Rows reserved for x at the top of every output column: PreallocationStrategy(P) (DLRM.jl
+# builds it as PreallocationStrategy{Float32}(feature_size), src/DLRM.jl:95; the package is
+# un-vendored, so its one integer field is read without naming it).
+prealloc_rows(s::PreallocationStrategy) =
+    something((getfield(s, f) for f in fieldnames(typeof(s)) if getfield(s, f) isa Integer)..., 0)
+
+function _maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse, P::Integer) where {D,T}
     ctx = first(tables).data.ctx
     idx = sparse isa PackedIndices ? sparse : pack(ctx, sparse)
-    P = D                                                           # rows 1:P reserved for x
     ys = DeviceMatrix{T}(ctx, P + D * length(tables), idx.batch)
     check(ctx, ccall((:dlrm_maplookup, libdlrm), Cint,
                      (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint, Ptr{Cvoid}, Int64, Int64),
@@ -176,26 +182,69 @@ function _maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse)
     return ys, idx
 end
 
-EmbeddingTables.maplookup(::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding}, sparse) =
-    first(_maplookup(tables, sparse))
+EmbeddingTables.maplookup(s::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding}, sparse) =
+    first(_maplookup(tables, sparse, prealloc_rows(s)))
 
-# The gradient of the lookup is the dt the interaction backward wrote; SparseEmbeddingUpdate
-# just names (dt, its row offset, the indices) so update! can hand them to the kernel.
-struct HipEmbeddingUpdate
-    dt::DeviceMatrix{Float32}
-    offset::Int
-    indices::PackedIndices
+# DefaultStrategy: one D x B matrix per table (test/model/embedding_update.jl:31, model.jl:155)
+function EmbeddingTables.maplookup(::DefaultStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}}, sparse) where {D}
+    ys = Array(first(_maplookup(tables, sparse, 0)))
+    return [ys[(D * (t - 1) + 1):(D * t), :] for t in eachindex(tables)]
 end
 
+# The maplookup pullback hands update! one SparseEmbeddingUpdate per table (DLRMGrads.embeddings
+# is a Vector{SparseEmbeddingUpdate}, src/train/train.jl:141-145, filled by append!, :183).  Its
+# delta is a (D x B) row block of the dt the interaction backward left in HBM and its indices
+# are the table's row of the packed device indices -- views, no copies -- built with the same
+# constructor DLRM.jl uses (SparseEmbeddingUpdate{Static{D}}(delta, indices), src/playground.jl:44).
+struct HipDelta <: AbstractMatrix{Float32}
+    dt::DeviceMatrix{Float32}
+    offset::Int      # first row of this table's block in every dt column (0-based)
+    D::Int
+end
+Base.size(d::HipDelta) = (d.D, size(d.dt, 2))
+Base.getindex(::HipDelta, ::Int...) = error("HipDelta lives in HBM; EmbeddingTables.uncompress copies it")
+
+struct HipIndices <: AbstractMatrix{Int32}
+    idx::PackedIndices
+    table::Int       # 1-based
+end
+Base.size(i::HipIndices) = (i.idx.lookups, i.idx.batch)      # L x B, sample-major (criteo.jl:551-557)
+Base.getindex(::HipIndices, ::Int...) = error("HipIndices live in HBM")
+
+const HipUpdate{D} = SparseEmbeddingUpdate{Static{D},HipDelta,HipIndices}
+hip_delta(u::SparseEmbeddingUpdate) = u.delta::HipDelta        # EmbeddingTables' field names
+hip_indices(u::SparseEmbeddingUpdate) = u.indices::HipIndices
+
 function ChainRulesCore.rrule(
-    ::typeof(maplookup), strategy::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding}, sparse
-)
-    ys, idx = _maplookup(tables, sparse)
-    D = featuresize(first(tables))
-    # one entry per table (grads.embeddings is a Vector, src/train/train.jl:144); all of them
-    # view the same dt: table t's rows sit at offset D + (t-1)*D of every dt column
-    pullback(dt) = (NoTangent(), NoTangent(), [HipEmbeddingUpdate(dt, D, idx) for _ in tables], NoTangent())
-    return ys, pullback
+    ::typeof(maplookup), strategy::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}}, sparse
+) where {D}
+    P = prealloc_rows(strategy)
+    ys, idx = _maplookup(tables, sparse, P)
+    function maplookup_pullback(dt)
+        dt isa DeviceMatrix{Float32} || throw(ArgumentError("the cotangent of ys is the dt of HipDotInteraction's pullback"))
+        ups = [SparseEmbeddingUpdate{Static{D}}(HipDelta(dt, P + (t - 1) * D, D), HipIndices(idx, t))
+               for t in eachindex(tables)]
+        return (NoTangent(), NoTangent(), ups, NoTangent())
+    end
+    return ys, maplookup_pullback
+end
+
+# uncompress(update, nrows) (test/train/backprop.jl:156): the dense D x N gradient, as
+# update!(Descent(-1)) of one zero table with the same deterministic kernel.
+function EmbeddingTables.uncompress(u::SparseEmbeddingUpdate{Static{D},HipDelta,HipIndices}, nrows::Integer) where {D}
+    δ, ix = hip_delta(u), hip_indices(u)
+    ctx = δ.dt.ctx
+    table = HipEmbedding(ctx, zeros(Float32, D, nrows))
+    L, B = ix.idx.lookups, ix.idx.batch
+    indexer = HipIndexer(ctx, 1, B * L)
+    row0 = Ptr{Int32}(ix.idx.data.ptr) + sizeof(Int32) * B * L * (ix.table - 1)   # this table's index row
+    check(ctx, ccall((:dlrm_sgd_update, libdlrm), Cint,
+                     (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cuint, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint,
+                      Ptr{Cvoid}, Cint, Int64, Int64, Cfloat),
+                     ctx.ptr, tableset([table]), indexer.ptr, Cuint(0), row0, DLRM_I32, B * L, 1, B, L,
+                     δ.dt.ptr, DLRM_F32, size(δ.dt, 1), δ.offset, -1.0f0))
+    check_bounds(ctx)
+    return Array(table.data)
 end
 
 #####
@@ -214,10 +263,10 @@ function interaction_sizes(d, F, pad_to)
     return padded, padded - width
 end
 
-function (dot::HipDotInteraction)(x::AbstractMatrix{T}, ys::DeviceMatrix{T}) where {T}
+function _interact(dot::HipDotInteraction, x::AbstractMatrix{T}, ys::DeviceMatrix{T}) where {T}
     d, B = size(x)
     F = size(ys, 1) ÷ d
-    xd = x isa DeviceMatrix ? x : upload!(DeviceMatrix{T}(dot.ctx, d, B), x)   # bottom MLP output
+    xd = x isa DeviceMatrix ? x : upload!(DeviceMatrix{T}(dot.ctx, d, B), Matrix{T}(x))   # bottom MLP output
     width, padding = interaction_sizes(d, F, dot.pad_to)
     out = DeviceMatrix{T}(dot.ctx, width, B)
     check(dot.ctx, ccall((:dlrm_interact_fwd, libdlrm), Cint,
@@ -226,18 +275,29 @@ function (dot::HipDotInteraction)(x::AbstractMatrix{T}, ys::DeviceMatrix{T}) whe
     return Array(out), padding                                     # the top MLP runs on the CPU
 end
 
-function ChainRulesCore.rrule(dot::HipDotInteraction, x::AbstractMatrix{T}, ys::DeviceMatrix{T}) where {T}
-    out, padding = dot(x, ys)
+# (dot::DotInteraction)(x, ys; return_t) (src/model/interact.jl:394-411): `out`, or with
+# return_t = true `(out, T, padding)` -- T is ys itself (x copied into its top rows).
+function (dot::HipDotInteraction)(x::AbstractMatrix{T}, ys::DeviceMatrix{T}; return_t = false) where {T}
+    out, padding = _interact(dot, x, ys)
+    return return_t ? (out, ys, padding) : out
+end
+# the bottom MLP's output is a OneDNN.Memory (interact.jl:390-392)
+(dot::HipDotInteraction)(x::OneDNN.Memory, ys::DeviceMatrix; kw...) = dot(OneDNN.materialize(x), ys; kw...)
+
+function ChainRulesCore.rrule(dot::HipDotInteraction, X, ys::DeviceMatrix{T}) where {T}
+    x = X isa OneDNN.Memory ? OneDNN.materialize(X) : X
+    out, padding = _interact(dot, x, ys)
     d, B = size(x)
     F = size(ys, 1) ÷ d
     function dot_pullback(Δ)
-        Δd = upload!(DeviceMatrix{T}(dot.ctx, size(Δ)...), Matrix{T}(Δ))
+        Δh = Δ isa OneDNN.Memory ? OneDNN.materialize(Δ) : Δ
+        Δd = upload!(DeviceMatrix{T}(dot.ctx, size(Δh)...), Matrix{T}(Δh))
         dx = DeviceMatrix{Float32}(dot.ctx, d, B)
         dt = DeviceMatrix{Float32}(dot.ctx, F * d, B)               # x rows included, as dot_back
         check(dot.ctx, ccall((:dlrm_interact_bwd, libdlrm), Cint,
                              (Ptr{Cvoid}, Cint, Cint, Cint, Cint, Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64,
                               Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64),
-                             dot.ctx.ptr, dtype_code(T), d, F, B, Δd.ptr, size(Δ, 1), padding, ys.ptr, size(ys, 1),
+                             dot.ctx.ptr, dtype_code(T), d, F, B, Δd.ptr, size(Δh, 1), padding, ys.ptr, size(ys, 1),
                              dx.ptr, d, dt.ptr, F * d))
         return (NoTangent(), Array(dx), dt)
     end
@@ -270,19 +330,28 @@ end
 const INDEXERS = IdDict{Any,HipIndexer}()
 
 # `num_splits` / `nthreads` tune the CPU scatter; the GPU kernel has its own decomposition.
+# Dispatch is on the table type: `custom_update!` (src/train/train.jl:283-290) passes the
+# Vector{SparseEmbeddingUpdate} that DLRMGrads gathered.
 function EmbeddingTables.update!(
-    opt, tables::AbstractVector{<:HipEmbedding{Static{D}}}, grads::AbstractVector{HipEmbeddingUpdate},
+    opt, tables::AbstractVector{<:HipEmbedding{Static{D}}}, grads::AbstractVector{<:SparseEmbeddingUpdate},
     indexers; num_splits = 8, nthreads = Threads.nthreads()
 ) where {D}
-    g = first(grads)           # one dt buffer and one packed index set serve every table
-    ctx = g.dt.ctx
-    idx = g.indices
+    length(grads) == length(tables) || throw(ArgumentError("one SparseEmbeddingUpdate per table"))
+    δ1, ix1 = hip_delta(first(grads)), hip_indices(first(grads))
+    # one dt buffer and one packed index set serve every table: table t's block sits D rows after t-1's
+    for (t, g) in enumerate(grads)
+        δ, ix = hip_delta(g), hip_indices(g)
+        (δ.dt === δ1.dt && δ.offset == δ1.offset + (t - 1) * D && ix.idx === ix1.idx && ix.table == t) ||
+            throw(ArgumentError("update! expects the per-table views of one maplookup pullback"))
+    end
+    ctx, idx = δ1.dt.ctx, ix1.idx
     ix = get!(() -> HipIndexer(ctx, length(tables), idx.batch * idx.lookups), INDEXERS, indexers)
     check(ctx, ccall((:dlrm_sgd_update, libdlrm), Cint,
                      (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cuint, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint,
                       Ptr{Cvoid}, Cint, Int64, Int64, Cfloat),
-                     ctx.ptr, tableset(tables), ix.ptr, 0, idx.data.ptr, DLRM_I32, idx.batch * idx.lookups, 1,
-                     idx.batch, idx.lookups, g.dt.ptr, DLRM_F32, size(g.dt, 1), g.offset, opt.eta))
+                     ctx.ptr, tableset(tables), ix.ptr, Cuint(0), idx.data.ptr, DLRM_I32, idx.batch * idx.lookups, 1,
+                     idx.batch, idx.lookups, δ1.dt.ptr, DLRM_F32, size(δ1.dt, 1), δ1.offset, opt.eta))
+    check_bounds(ctx)     # BoundsError, as the reference's gather throws (no row was written)
     return nothing
 end
 
@@ -343,6 +412,48 @@ function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}) where {T}
                         st.lr, Cuint(0)))
     return Array(st.dx)
 end
+
+#####
+##### Table-sharded exchange (one Julia process per GPU): dlrm_comm_* + dlrm_alltoall_fwd / _bwd
+#####
+
+"""
+    Comm(ctx, id::Vector{UInt8}, rank, nranks)
+
+An RCCL communicator over the node's GPUs.  `comm_unique_id()` on one rank gives the 128-byte
+`id` every rank passes in (distribute it with `Distributed` / MPI / a file).  `alltoall_fwd!`
+sends this rank's looked-up vectors of every rank's samples (`send`: [nranks][T_me][B][D]) and
+receives every owner's vectors of its own samples (`recv`: [src][T_src][B][D]); `alltoall_bwd!`
+returns the fp32 gradient rows to the tables' owners.  Both run on the ctx stream.
+"""
+mutable struct Comm
+    ctx::Context
+    ptr::Ptr{Cvoid}
+    counts::Vector{Cint}     # tables owned by each rank
+    function Comm(ctx::Context, id::Vector{UInt8}, rank::Integer, nranks::Integer, counts::AbstractVector{<:Integer})
+        length(id) == 128 || throw(ArgumentError("a communicator id has 128 bytes"))
+        out = Ref{Ptr{Cvoid}}(C_NULL)
+        check(ctx, ccall((:dlrm_comm_init, libdlrm), Cint, (Ptr{Cvoid}, Ptr{UInt8}, Cint, Cint, Ref{Ptr{Cvoid}}),
+                         ctx.ptr, id, rank, nranks, out))
+        c = new(ctx, out[], Cint.(counts))
+        finalizer(x -> ccall((:dlrm_comm_destroy, libdlrm), Cint, (Ptr{Cvoid},), x.ptr), c)
+        return c
+    end
+end
+function comm_unique_id()
+    id = zeros(UInt8, 128)
+    rc = ccall((:dlrm_comm_unique_id, libdlrm), Cint, (Ptr{UInt8},), id)
+    rc == 0 || throw(DLRMError(rc, "dlrm_comm_unique_id"))
+    return id
+end
+alltoall_fwd!(c::Comm, send::DeviceMatrix{T}, recv::DeviceMatrix{T}, D::Integer, B::Integer) where {T} =
+    check(c.ctx, ccall((:dlrm_alltoall_fwd, libdlrm), Cint,
+                       (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Cint, Cint, Ptr{Cint}, Ptr{Cvoid}, Ptr{Cvoid}),
+                       c.ctx.ptr, c.ptr, dtype_code(T), D, B, c.counts, send.ptr, recv.ptr))
+alltoall_bwd!(c::Comm, gsend::DeviceMatrix{Float32}, grecv::DeviceMatrix{Float32}, D::Integer, B::Integer) =
+    check(c.ctx, ccall((:dlrm_alltoall_bwd, libdlrm), Cint,
+                       (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Cint, Ptr{Cint}, Ptr{Cvoid}, Ptr{Cvoid}),
+                       c.ctx.ptr, c.ptr, D, B, c.counts, gsend.ptr, grecv.ptr))
 
 #####
 ##### DACLoader replacement (src/data/criteo.jl:309-340): records uploaded raw, load! on the GPU

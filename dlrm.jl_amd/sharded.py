@@ -26,9 +26,12 @@ way moves the looked-up vectors to the ranks that own the samples, and their gra
 All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-ABI kernels)
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
 = RCCL over xGMI on MI355X) carries the two all-to-alls (uneven table counts per rank: the
-split-size form of all_to_all_single).  The bench replays the compute between the two
-collectives as hipGraphs (`capture`); the collectives themselves are launched eagerly.
+split-size form of all_to_all_single), or, with exchange="abi", the library's own RCCL
+communicator (dlrm_alltoall_fwd / _bwd, dlrm.jl_amd/comm.py).  The bench replays the compute
+between the two collectives as hipGraphs (`capture`); the collectives are launched eagerly.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -158,7 +161,7 @@ class HipShardOps:
 class ShardedHotPath:
     """One step of the table-sharded hot path on this rank (see module docstring)."""
 
-    def __init__(self, ops, partition, rank, batch_local, dim, lookups, dtype, device, group=None):
+    def __init__(self, ops, partition, rank, batch_local, dim, lookups, dtype, device, group=None, exchange=None):
         self.ops, self.part, self.rank = ops, partition, rank
         self.world = partition.world
         self.B, self.D, self.L = batch_local, dim, lookups
@@ -196,6 +199,16 @@ class ShardedHotPath:
         self.gs_base = torch.tensor(base, dtype=torch.int64, device=dev)
         self.gs_ld = torch.tensor(ld, dtype=torch.int64, device=dev)
         ops.bind_recv(self.recv_tables)
+        # the exchange: torch.distributed (default; backend "nccl" = RCCL) or the library's own RCCL
+        # communicator (exchange="abi" / DLRM_EXCHANGE=abi: dlrm_alltoall_fwd / _bwd, as a Julia
+        # process per GPU would drive it)
+        exchange = exchange or os.environ.get("DLRM_EXCHANGE", "torch")
+        self.comm = None
+        if exchange == "abi":
+            from .comm import CommExchange
+            self.comm = CommExchange(rank, self.world, dev, group=group)
+        elif exchange != "torch":
+            raise ValueError(f"exchange must be 'torch' or 'abi', not {exchange!r}")
         self._graphs = None
         self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
 
@@ -211,6 +224,9 @@ class ShardedHotPath:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def exchange_fwd(self):
+        if self.comm is not None:
+            self.comm.alltoall_fwd(self.send, self.recv, self.D, self.B, self.part.counts)
+            return
         self._a2a(self.recv, self.send, self.fwd_out_splits, self.fwd_in_splits)
 
     def pack_grad(self):
@@ -219,6 +235,9 @@ class ShardedHotPath:
                               self.D)
 
     def exchange_bwd(self):
+        if self.comm is not None:
+            self.comm.alltoall_bwd(self.gsend, self.grecv, self.D, self.B, self.part.counts)
+            return
         self._a2a(self.grecv, self.gsend, self.bwd_out_splits, self.bwd_in_splits)
 
     # ---- the step, as three compute segments around the two exchanges

@@ -46,15 +46,27 @@ class SparseEmbeddingUpdate:
         return self.grad[:, self.grad_offset:self.grad_offset + self.featuresize]
 
     def uncompress(self, nrows, *, index_base=1):
-        """uncompress(update, nrows) (test/train/backprop.jl:156): dense [nrows][D] scatter-add.
-        A plain torch scatter for tests/inspection; the training path never materialises it."""
-        idx = self.indices.data[self.table_index].to(torch.int64) - index_base
-        L = self.indices.L
-        g = self.delta.to(torch.float32)
-        if L > 1:
-            g = g.repeat_interleave(L, dim=0)
-        out = torch.zeros((nrows, self.featuresize), dtype=torch.float32, device=g.device)
-        out.index_add_(0, idx, g)
+        """uncompress(update, nrows) (test/train/backprop.jl:156): the dense [nrows][D] gradient,
+        Σ of delta rows per index (pooled bags: a bag's row counts once per lookup).  It is
+        update!(Descent(-1)) into a zero table -- the same deterministic HIP indexer + apply, so the
+        sum per row runs in ascending position order, fp32."""
+        if self.indices.data.device.type != "cuda":
+            raise ValueError("uncompress runs on the GPU (the indices must be device tensors)")
+        dev = self.indices.data.device
+        out = torch.zeros((nrows, self.featuresize), dtype=torch.float32, device=dev)
+        ts = EmbeddingTableSet([out])
+        one = PackedIndices(self.indices.data[self.table_index:self.table_index + 1].reshape(
+            1, self.indices.B, self.indices.L))
+        g = self.grad
+        if g.stride(1) != 1:
+            raise ValueError("gradient rows must be contiguous")
+        require_device(g, dev, "gradient")
+        ix = SparseIndexer(1, one.B * one.L, dev)
+        ctx = ts.ctx
+        ctx.check(ctx.lib.dlrm_sgd_update(ctx.bind(), ts.handle, ix.handle, 0, ptr(one.data), one.itype, one.stride,
+                                          index_base, one.B, one.L, ptr(g), dtype_code(g.dtype), g.stride(0),
+                                          self.grad_offset, -1.0))
+        ctx.check_bounds()
         return out
 
 

@@ -14,6 +14,9 @@
  *   dlrm_interact_bwd     dot_back / process_batches_back        src/model/interact.jl:415-489
  *                         (fused unpack :154-173, gemmavx! :318-326, sumavx :329-336)
  *   dlrm_indexer_*        EmbeddingTables.SparseIndexer()        src/train/train.jl:276-281
+ *   dlrm_triangular_slice(_back), dlrm_self_batched_mul(_back)
+ *                         Implementation 2 of the interaction (dot_interaction, the default of
+ *                         dlrm(), model.jl:180): src/model/interact.jl:176-215, :503-551
  *   dlrm_sgd_update       EmbeddingTables.update!(Descent(lr), tables, grads, indexers;
  *                         num_splits, nthreads)                  src/train/train.jl:283-290
  *                         (grads = maplookup pullback = SparseEmbeddingUpdate views of dt,
@@ -155,6 +158,31 @@ int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tables,
                              const void* x, int64_t x_ld, void* ys, int64_t ys_ld,
                              void* out, int64_t out_ld, int padding);
 
+/* ---- Implementation 2 of the interaction, as separate operators --------------------------
+ * dot_interaction (src/model/interact.jl:503-517; the default of dlrm(), model.jl:180) composes
+ * fast_vcat + self_batched_mul + triangular_slice; dlrm_interact_fwd / dlrm_interact_bwd are that
+ * composition and its pullback in one launch each.  These are the pieces and their rrules, for
+ * callers that compose them as the reference does.  Layouts: Z, dZ (sz, sz, B) = [B][sz][sz]
+ * (batch stride given, element [b][col][row] = Julia z[row, col, b]); the slice (ncols, B) = [B][ld];
+ * T (d, F, B) = [B][F][d] (batch stride t_ld).
+ * dlrm_triangular_slice       triangular_slice (:176-191): out[b][col(col-1)/2 + row] = z[b][col][row],
+ *                             row < col (triangular_slice_kernel! order, :64-75).  Bit-exact copy.
+ * dlrm_triangular_slice_back  its rrule (:193-215): a[b][col][row] = dy[b][col(col-1)/2 + row] for
+ *                             row < col, 0 elsewhere (triangular_slice_back_kernel!, :104-120);
+ *                             symmetric != 0: also the lower triangle (the fused add-transpose form,
+ *                             :150-171).  Bit-exact.
+ * dlrm_self_batched_mul       self_batched_mul (:526-537): z[b] = T_b^T T_b (full, F x F), fp32
+ *                             accumulation, stored in dtype.  F <= 90.
+ * dlrm_self_batched_mul_back  its rrule (:539-551): dt[b] = T_b (dz_b + dz_b^T), fp32 out.  F <= 90. */
+int dlrm_triangular_slice(dlrm_ctx* ctx, int dtype, int sz, int batch, const void* z, int64_t z_batch_stride,
+                          void* out, int64_t out_ld);
+int dlrm_triangular_slice_back(dlrm_ctx* ctx, int dtype, int sz, int batch, const void* dy, int64_t dy_ld, void* a,
+                               int64_t a_batch_stride, int symmetric);
+int dlrm_self_batched_mul(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* t, int64_t t_ld,
+                          void* z, int64_t z_batch_stride);
+int dlrm_self_batched_mul_back(dlrm_ctx* ctx, int dtype, int d, int num_features, int batch, const void* t,
+                               int64_t t_ld, const void* dz, int64_t dz_batch_stride, float* dt, int64_t dt_ld);
+
 /* dot_back(dot, dout, t, d, padding): S_b = symmetric zero-diagonal unpack of
  * dout[b][d : d + F(F-1)/2];  dt[b] = S_b T_b  ([F][d], fp32, x-rows included as the
  * reference returns them);  dx[b] = dout[b][0:d] + dt[b][0:d]  (fp32).
@@ -244,6 +272,28 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
                   const void* indices, int itype, int64_t table_stride, int index_base, int batch,
                   const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,
                   float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr, unsigned flags);
+
+/* ---- table-sharded exchange over RCCL ------------------------------------
+ * DLRM.jl is one process: maplookup hands its output straight to the interaction (model.jl:161-163).
+ * With the tables sharded by table over the GPUs of a node (one host process per GPU), that hand-off
+ * is an all-to-all each way.  table_counts[p] = tables owned by rank p (host array, nranks entries);
+ * B = samples per rank; blocks are contiguous and in owner order (exchange layout of
+ * dlrm_maplookup_blocked / dlrm_scatter_rows):
+ *   dlrm_alltoall_fwd: send [nranks][T_me][B][dim] (dtype) -> recv [src][T_src][B][dim]
+ *   dlrm_alltoall_bwd: gsend [owner][B][T_owner][dim] (fp32) -> grecv [src][B][T_me][dim]
+ *                      (= the [nranks*B][T_me*dim] gradient of this rank's tables for the global batch)
+ * dlrm_comm_unique_id fills DLRM_COMM_ID_BYTES bytes on one rank; the caller hands them to every
+ * rank (e.g. Julia's Distributed, MPI or a file), which calls dlrm_comm_init with its rank.  Both
+ * exchanges are asynchronous on the ctx stream (RCCL group of one send + one receive per peer). */
+#define DLRM_COMM_ID_BYTES 128
+typedef struct dlrm_comm dlrm_comm;
+int dlrm_comm_unique_id(void* id);
+int dlrm_comm_init(dlrm_ctx* ctx, const void* id, int rank, int nranks, dlrm_comm** out);
+int dlrm_comm_destroy(dlrm_comm* comm);
+int dlrm_alltoall_fwd(dlrm_ctx* ctx, dlrm_comm* comm, int dtype, int dim, int batch_local, const int* table_counts,
+                      const void* send, void* recv);
+int dlrm_alltoall_bwd(dlrm_ctx* ctx, dlrm_comm* comm, int dim, int batch_local, const int* table_counts,
+                      const float* gsend, float* grecv);
 
 /* ---- dense half of the training step (the GEMMs stay on hipBLASLt) --------
  * dlrm_bce_head: one launch for the top MLP's head after its last GEMM, replacing

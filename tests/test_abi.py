@@ -72,3 +72,73 @@ def test_julia_shim_binds_only_declared_entry_points():
     assert called, "no ccall found"
     missing = called - set(_lib.header_functions())
     assert not missing, missing
+
+
+def _julia_ccalls(text):
+    """(name, return type, [argument types], [arguments]) of every ccall((:dlrm_*, libdlrm), ...)."""
+    out = []
+    for m in re.finditer(r"ccall\(\(:(dlrm_[a-z0-9_]+),\s*libdlrm\),", text):
+        # split the rest of the ccall at top-level commas
+        i, depth, parts, cur = m.end(), 1, [], ""
+        while depth > 0:
+            ch = text[i]
+            if ch in "({[":
+                depth += 1
+            elif ch in ")}]":
+                depth -= 1
+            if depth == 1 and ch == ",":
+                parts.append(cur.strip())
+                cur = ""
+            elif depth > 0:
+                cur += ch
+            i += 1
+        parts.append(cur.strip())
+        ret, tys, args = parts[0], parts[1], parts[2:]
+        assert tys.startswith("(") and tys.endswith(")"), (m.group(1), tys)
+        inner, depth, cur, types = tys[1:-1], 0, "", []
+        for ch in inner + ",":
+            if ch in "{(":
+                depth += 1
+            elif ch in "})":
+                depth -= 1
+            if ch == "," and depth == 0:
+                if cur.strip():
+                    types.append(cur.strip())
+                cur = ""
+            else:
+                cur += ch
+        out.append((m.group(1), ret, types, args))
+    return out
+
+
+def _c_kind(param):
+    p = re.sub(r"\b(const|struct)\b", "", param).strip()
+    if "*" in p:
+        return "ptr"
+    base = p.rsplit(None, 1)[0] if len(p.split()) > 1 else p
+    return {"int": "i32", "unsigned": "u32", "int64_t": "i64", "size_t": "usize", "float": "f32"}[base.strip()]
+
+
+def _julia_kind(t):
+    if t.startswith(("Ptr{", "Ref{")) or t in ("Cstring",):
+        return "ptr"
+    return {"Cint": "i32", "Cuint": "u32", "Int64": "i64", "Csize_t": "usize", "Cfloat": "f32"}[t]
+
+
+def test_julia_shim_ccall_types_match_header(pkg):
+    """Every ccall in the Julia shim passes as many arguments as the C prototype has, each with a
+    Julia type of the same C kind (pointer / int / unsigned / int64 / size_t / float), and
+    returns Cint (or Cstring for dlrm_last_error)."""
+    text = open(os.path.join(ROOT, "dlrm.jl_amd", "julia", "DLRMHip.jl")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", open(pkg._lib.HEADER).read(), flags=re.S)
+    calls = _julia_ccalls(text)
+    assert len(calls) >= 20
+    for name, ret, types, args in calls:
+        m = re.search(r"\b(?:int|const char\*)\s+" + name + r"\s*\(([^)]*)\)", hdr)
+        assert m, f"{name}: no prototype in the header"
+        params = [q for q in m.group(1).split(",") if q.strip() and q.strip() != "void"]
+        assert len(types) == len(params), (name, types, params)
+        assert len(args) == len(types), (name, "argument count != type tuple", args)
+        for jt, cp in zip(types, params):
+            assert _julia_kind(jt) == _c_kind(cp), (name, jt, cp)
+        assert ret == ("Cstring" if name == "dlrm_last_error" else "Cint"), (name, ret)

@@ -1,0 +1,220 @@
+"""Parity at the BASELINE.json configurations the metric test does not cover.
+
+  configs[2]  26 Criteo-Kaggle tables x 128 bf16, B = 8192 (the hash-built indexer, MFMA bf16)
+  configs[3]  Criteo-Terabyte rows (882.8M, 226 GB bf16 on one GPU), Zipf(1.05) hot rows
+  configs[4]  pooled bags: 64 tables x 256 fp32, L = 10, Zipf(1.2) hot rows
+
+The C oracle (oracle/dlrm_oracle.c) cannot hold 9-226 GB of tables, but a training step reads
+and writes only the rows its indices touch: `compact()` copies those rows out of the device
+tables, renumbers the indices, and the oracle runs the same step on the compact tables.  The
+forward output, dx and every touched row after the update are compared; untouched rows are
+checked to be unchanged on the device.  Where even that is too large, size-independent
+properties are used: row-encoded gathers (bit-exact), exact integer-gradient updates.
+Reference semantics: sum pooling, sample-major bags (src/data/criteo.jl:551-557); table sizes
+src/data/criteo.jl:350-406."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16_bits(t):
+    return t.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def host_rows(t, rows):
+    """rows of a device table as a host array (float32, or bf16 bit patterns)."""
+    sel = t.index_select(0, torch.from_numpy(rows).to(t.device))
+    return sel.cpu().numpy() if t.dtype == torch.float32 else bf16_bits(sel)
+
+
+def compact(tables, idx_np):
+    """(unique rows per table, compact host tables, renumbered indices [T][N] int64)."""
+    uniq, comp, ridx = [], [], np.empty_like(idx_np, dtype=np.int64)
+    for t, tab in enumerate(tables):
+        u, inv = np.unique(idx_np[t], return_inverse=True)
+        uniq.append(u)
+        comp.append(host_rows(tab, u))
+        ridx[t] = inv
+    return uniq, comp, ridx
+
+
+def to_f32(a):
+    return oracle.bf16_to_f32(a) if a.dtype == np.uint16 else a
+
+
+def zipf_indices(pkg, rng, rows, n, s):
+    return np.stack([pkg.zipf_rows(rng, r, n, s, pkg.zipf_perm(rng, r)) for r in rows]).astype(np.int64)
+
+
+def run_step_vs_oracle(pkg, gpu, tables, idx_np, B, L, lr, dtype, seed, hot_kw=None):
+    """One HotPath training step on the device tables against the oracle's step on their touched
+    rows.  Returns nothing; asserts out, dx, touched rows after the update, untouched rows."""
+    T, D = len(tables), tables[0].shape[1]
+    F = T + 1
+    uniq, comp, ridx = compact(tables, idx_np)
+    before = [t.clone() for t in tables] if sum(t.numel() for t in tables) * 2 < 40e9 else None
+    rng = np.random.default_rng(seed)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(dtype).to(gpu)
+    ts = pkg.EmbeddingTableSet(tables)
+    hp = pkg.HotPath(ts, B, L, lr=lr, index_base=0, **(hot_kw or {}))
+    dout = torch.from_numpy((rng.standard_normal((B, hp.width)) * 1e-2).astype(np.float32)).to(dtype).to(gpu)
+    p = pkg.PackedIndices(torch.from_numpy(idx_np).to(torch.int32).to(gpu).reshape(T, B, L))
+    hp.validate(x, p, dout)
+    hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    # the oracle's step on the compact tables
+    xh = x.cpu().numpy() if dtype == torch.float32 else bf16_bits(x)
+    dh = dout.cpu().numpy() if dtype == torch.float32 else bf16_bits(dout)
+    ys = np.zeros((B, F * D), dtype=xh.dtype)
+    oracle.maplookup(comp, ridx, 0, B, L, ys, D)
+    out = oracle.interact_fwd(xh, ys, F, hp.padding)
+    dx, dt = oracle.interact_bwd(dh, ys, D, F, hp.padding)
+    oracle.sgd_update(comp, ridx, 0, B, L, dt, D, lr)
+    bf = dtype == torch.bfloat16
+    got_out = hp.out.float().cpu().numpy()
+    if bf:  # one bf16 rounding of an fp32 sum that may differ in order: 2 ulp of bf16
+        err = np.abs(got_out - to_f32(out))
+        assert (err <= 2.0 ** -7 * np.abs(to_f32(out)) + 1e-6).all(), ("out", err.max())
+    else:
+        assert_close(got_out, out, rtol=1e-5, scale=np.abs(out).max(), what="out")
+    assert_close(hp.dx.cpu().numpy(), dx, rtol=1e-4 if bf else 1e-5, scale=np.abs(dx).max(), what="dx")
+    for t, tab in enumerate(tables):
+        got = to_f32(host_rows(tab, uniq[t]))
+        want = to_f32(comp[t])
+        if bf:  # the same fp32 update, each side rounded once to bf16: at most 1 ulp (2^-7 relative) apart
+            err = np.abs(got - want)
+            assert (err <= 2.0 ** -7 * np.abs(want) + 1e-30).all(), (t, err.max())
+        else:
+            g = np.abs(to_f32(host_rows(before[t], uniq[t])) - want) if before is not None else np.abs(want)
+            assert_close(got, want, rtol=1e-5, scale=g.max() + 1e-6, what=f"table {t} rows")
+        if before is not None:  # every other row unchanged
+            mask = torch.ones(tab.shape[0], dtype=torch.bool, device=gpu)
+            mask[torch.from_numpy(uniq[t]).to(gpu)] = False
+            assert torch.equal(tab[mask], before[t][mask]), f"table {t}: an untouched row changed"
+    return hp
+
+
+# ---------------------------------------------------------------------------- configs[2]
+def test_kaggle_bf16_b8192_step_vs_oracle(pkg, gpu):
+    """configs[2]: the full Kaggle tables (33.8M rows x 128 bf16 = 8.6 GB), B = 8192, uniform
+    indices: the step (hash indexer on the side stream, bf16 MFMA interaction, once-hit rows
+    updated in the backward) against the oracle on the touched rows."""
+    rows = pkg.KAGGLE_EMBEDDING_SIZES
+    D, B = 128, 8192
+    g = torch.Generator(device=gpu).manual_seed(11)
+    tables = [torch.empty((n, D), dtype=torch.bfloat16, device=gpu).uniform_(-n ** -0.5, n ** -0.5, generator=g)
+              for n in rows]
+    rng = np.random.default_rng(12)
+    idx = np.stack([rng.integers(0, n, size=B) for n in rows]).astype(np.int64)
+    hp = run_step_vs_oracle(pkg, gpu, tables, idx, B, 1, 0.05, torch.bfloat16, seed=13)
+    assert hp.step_api  # the bench's step form
+
+
+# ---------------------------------------------------------------------------- configs[4]
+def test_pooled_64x256_l10_zipf_step_vs_oracle(pkg, gpu):
+    """configs[4] at 100k rows per table (the oracle's size): 64 tables x 256 fp32, L = 10 sum-pooled
+    bags, Zipf(1.2) hot rows, B = 2048 -- the bench's pooled path (many-wave pooled gather, the
+    interaction at d = 256 / F = 65, hash indexer, the hot-segment apply) against the oracle."""
+    rows = [100_000] * 64
+    D, B, L = 256, 2048, 10
+    g = torch.Generator(device=gpu).manual_seed(21)
+    tables = [torch.empty((n, D), device=gpu).uniform_(-n ** -0.5, n ** -0.5, generator=g) for n in rows]
+    rng = np.random.default_rng(22)
+    idx = zipf_indices(pkg, rng, rows, B * L, 1.2)
+    hp = run_step_vs_oracle(pkg, gpu, tables, idx, B, L, 0.05, torch.float32, seed=23)
+    assert hp.materialize_ys  # pooled bags keep ys (the bench's form)
+
+
+def test_pooled_full_size_properties(pkg, gpu):
+    """configs[4] at full size (64 x 1M x 256 fp32 = 65.5 GB): the pooled gather of row-encoded
+    tables is exact (a bag's L encoded rows sum without rounding), and an integer-gradient
+    update on zeroed tables equals the closed-form scatter-add bit for bit (each bag's gradient
+    counted once per lookup, duplicates within a bag included)."""
+    T, N, D, B, L = 64, 1_000_000, 256, 2048, 10
+    rng = np.random.default_rng(31)
+    idx = torch.from_numpy(zipf_indices(pkg, rng, [N] * T, B * L, 1.2)).to(torch.int32).to(gpu)
+    col = torch.arange(D, device=gpu, dtype=torch.float32)[None, :] / 256.0
+    tables = []
+    for t in range(T):  # value = (row mod 1021) + c/256 (+ nothing per table: sums stay < 2^14)
+        r = torch.arange(N, device=gpu, dtype=torch.float32).remainder_(1021.0)
+        tables.append((r[:, None] + col).contiguous())
+    ts = pkg.EmbeddingTableSet(tables)
+    p = pkg.PackedIndices(idx.reshape(T, B, L))
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, p, index_base=0)
+    want = idx.to(torch.float32).remainder(1021.0).reshape(T, B, L).sum(dim=2)  # [T][B], exact
+    want = want.T[:, :, None] + L * col[None, :, :]
+    assert torch.equal(ys[:, D:].reshape(B, T, D), want)
+    del ys
+    for t in tables:
+        t.zero_()
+    gi = torch.from_numpy(rng.integers(-4, 5, size=(B, T * D)).astype(np.float32)).to(gpu)
+    pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, gi), index_base=0)
+    for t in (0, 17, 63):
+        rows_t = idx[t].long()
+        u = torch.unique(rows_t)
+        ref = torch.zeros((N, D), dtype=torch.float64, device=gpu)
+        ref.index_add_(0, rows_t, gi[:, t * D:(t + 1) * D].double().repeat_interleave(L, dim=0))
+        assert torch.equal(tables[t][u], (-ref[u]).float())
+        nz = tables[t].abs().sum(dim=1) != 0
+        touched = torch.zeros(N, dtype=torch.bool, device=gpu)
+        touched[u] = True
+        assert not (nz & ~touched).any(), "a row no index touched was written"
+
+
+# ---------------------------------------------------------------------------- configs[3]
+def test_terabyte_bf16_full_size(pkg, gpu):
+    """configs[3] on one GPU: the 26 Criteo-Terabyte tables (882.8M rows x 128 bf16 = 226 GB,
+    criteo.jl:379-406).  (1) Row-encoded gather: columns 0-3 of row r hold its four bytes and
+    column 4 the table, so every gathered row identifies itself exactly (bf16 holds 0-255).
+    (2) A Zipf(1.05) training step (the bench's workload) against the oracle on its touched rows.
+    (3) An integer-gradient update on zeroed tables == the closed form, bit for bit."""
+    rows = pkg.TERABYTE_EMBEDDING_SIZES
+    T, D, B = len(rows), 128, 2048
+    if torch.cuda.get_device_properties(gpu).total_memory < sum(rows) * D * 2 + 20e9:
+        pytest.skip("needs a 288 GB MI355X")
+    tables = [torch.empty((n, D), dtype=torch.bfloat16, device=gpu) for n in rows]
+    chunk = 1 << 24
+    for t, (tab, n) in enumerate(zip(tables, rows)):
+        tab[:, 5:] = 1.0
+        for r0 in range(0, n, chunk):
+            r = torch.arange(r0, min(n, r0 + chunk), device=gpu, dtype=torch.int64)
+            for k in range(4):
+                tab[r0:r0 + len(r), k] = ((r >> (8 * k)) & 255).to(torch.bfloat16)
+            tab[r0:r0 + len(r), 4] = float(t)
+    rng = np.random.default_rng(41)
+    idx_np = zipf_indices(pkg, rng, rows, B, 1.05)
+    idx = torch.from_numpy(idx_np).to(torch.int32).to(gpu)
+    ts = pkg.EmbeddingTableSet(tables)
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, pkg.PackedIndices(idx), index_base=0)
+    got = ys[:, D:].reshape(B, T, D).float()
+    dec = sum(got[:, :, k].to(torch.int64) << (8 * k) for k in range(4))  # [B][T]
+    assert torch.equal(dec, idx.T.to(torch.int64))
+    assert torch.equal(got[:, :, 4], torch.arange(T, device=gpu, dtype=torch.float32)[None, :].expand(B, T))
+    del ys, got
+    # (2) the training step vs the oracle (fresh random rows where the step reads and writes)
+    g = torch.Generator(device=gpu).manual_seed(42)
+    for t, tab in enumerate(tables):
+        u = torch.unique(idx[t].long())
+        tab[u] = torch.empty((len(u), D), device=gpu).uniform_(-0.05, 0.05, generator=g).to(torch.bfloat16)
+    hp = run_step_vs_oracle(pkg, gpu, tables, idx_np, B, 1, 0.05, torch.bfloat16, seed=43)
+    del hp
+    # (3) exact integer-gradient update on zeroed tables
+    for tab in tables:
+        tab.zero_()
+    gi = torch.from_numpy(rng.integers(-4, 5, size=(B, T * D)).astype(np.float32)).to(gpu)
+    p = pkg.PackedIndices(idx)
+    pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, gi), index_base=0)
+    for t in (0, 5, 19, 25):  # 227.6M, 3, 292.8M (the largest) and 36 rows
+        rows_t = idx[t].long()
+        u = torch.unique(rows_t)
+        ref = torch.zeros((len(u), D), dtype=torch.float64, device=gpu)
+        ref.index_add_(0, torch.searchsorted(u, rows_t), gi[:, t * D:(t + 1) * D].double())
+        assert torch.equal(tables[t][u].float(), (-ref).float().to(torch.bfloat16).float())
+        nz = (tables[t] != 0).any(dim=1).nonzero().flatten()
+        assert torch.isin(nz, u).all(), "a row no index touched was written"

@@ -406,14 +406,44 @@ def test_sgd_update_integer_gradients_exact(pkg, gpu):
         assert np.array_equal(to_np_f32(ts[t].data), (-want).astype(np.float32))
 
 
-def test_update_bounds_error(pkg, gpu):
+@pytest.mark.parametrize("deterministic", [True, False])
+def test_update_bounds_error(pkg, gpu, deterministic):
+    """An out-of-range index: Julia's checked gather throws BoundsError at maplookup
+    (model.jl:161), before update!, so the tables stay untouched -- not even the valid index's
+    row is written.  After the error is reported the flag is clear and updates apply again."""
     ts = pkg.EmbeddingTableSet([torch.zeros((4, 16), device=gpu)])
     p = pkg.PackedIndices([torch.tensor([1, 5])])
     g = torch.ones((2, 16), device=gpu)
     with pytest.raises(pkg.BoundsError):
-        pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, g))
-    # the valid index was still applied, the invalid one skipped
-    assert to_np_f32(ts[0].data)[0].tolist() == [-1.0] * 16
+        pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, p, g), deterministic=deterministic)
+    assert not to_np_f32(ts[0].data).any()
+    ok = pkg.PackedIndices([torch.tensor([1, 1])])
+    pkg.update_(pkg.Descent(1.0), ts, pkg.maplookup_pullback(0, ts, ok, g), deterministic=deterministic)
+    ts.ctx.check_bounds()
+    assert to_np_f32(ts[0].data)[0].tolist() == [-2.0] * 16  # index_base 1: row 0, hit twice
+
+
+@pytest.mark.parametrize("B", [512, 6000])
+def test_step_bounds_error_leaves_tables(pkg, gpu, B):
+    """The training step (dlrm_step_fwd / dlrm_step_bwd, once-hit rows updated inside the backward)
+    with one out-of-range index: BoundsError, and no table row changes (the reference throws in
+    maplookup, model.jl:161, before any update!)."""
+    rng = np.random.default_rng(9)
+    rows = [5, 300, 100000]
+    D = 32
+    tabs = rand_tables(rng, rows, D)
+    idx_np = rand_indices(rng, rows, B, 1)
+    idx_np[2, B // 3] = rows[2] + 7  # out of range
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    hp = pkg.HotPath(ts, B, 1, lr=0.1, index_base=0)
+    p = pkg.PackedIndices(torch.from_numpy(idx_np).to(torch.int32).to(gpu).reshape(3, B, 1))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    dout = torch.from_numpy(rng.standard_normal((B, hp.width)).astype(np.float32)).to(gpu)
+    hp.step(x, p, dout)
+    with pytest.raises(pkg.BoundsError):
+        hp.check_bounds()
+    for t in range(3):
+        assert np.array_equal(to_np_f32(ts[t].data), tabs[t]), f"table {t} was written on a BoundsError step"
 
 
 # ------------------------------------------------------------------ the engine
@@ -533,7 +563,8 @@ def test_step_api_state_and_bounds(pkg, gpu):
     hp.step_bwd(dout, x=x, idx=p)
     torch.cuda.synchronize()
     hp.check_bounds()
-    # out-of-range: skipped everywhere, flagged once
+    # out-of-range: flagged; no table row is written (by the step or by the operators: the
+    # reference's gather throws before update!), and out / dx agree on the valid positions
     bad_np = idx_np.copy()
     bad_np[1, 5] = rows[1] + 3
     bad = pkg.PackedIndices(torch.from_numpy(bad_np).to(torch.int32).to(gpu))
@@ -656,7 +687,43 @@ def test_host_tensors_are_rejected_before_launch(pkg, gpu):
 
 
 # ------------------------------------------------------------------ sharded (2 ranks on one GPU)
-def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False):
+SHARD_CASES = {
+    "small": dict(rows=[3, 5000, 70, 100000, 11], D=32, B=64, L=2, zipf=None),
+    # Criteo-Terabyte's 26 row counts (criteo.jl:379-406) scaled by 1/20000 (floor 3), Zipf(1.05)
+    # hot rows, one-hot: TablePartition.fitting at a capacity the contiguous halves exceed
+    "terabyte-scaled": dict(rows=[max(3, n // 20000) for n in [
+        227605432, 39060, 17295, 7424, 20265, 3, 7122, 1543, 63, 130229467, 3067956, 405282, 10,
+        2209, 11938, 155, 4, 976, 14, 292775614, 40790948, 187188510, 590152, 12973, 108, 36]],
+        D=32, B=256, L=1, zipf=1.05),
+}
+
+
+def _shard_inputs(case, world):
+    c = SHARD_CASES[case]
+    rows, D, B, L = c["rows"], c["D"], c["B"], c["L"]
+    T, Bg = len(rows), B * world
+    rng = np.random.default_rng(7)
+    tabs = rand_tables(rng, rows, D)
+    idx = rand_indices(rng, rows, Bg, L, zipf=c["zipf"])
+    x = rng.standard_normal((Bg, D)).astype(np.float32)
+    F = T + 1
+    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
+    return rows, D, B, L, tabs, idx, x, dout
+
+
+def _shard_owners(case, owners, world):
+    if owners != "fitting":
+        return owners
+    from dlrm_jl_amd.sharded import TablePartition
+    c = SHARD_CASES[case]
+    rb = c["D"] * 4
+    cap = int(0.56 * sum(c["rows"]) * rb)  # the contiguous halves need ~0.59 of the bytes (as at full size)
+    part = TablePartition.fitting(c["rows"], world, rb, cap)
+    assert not part.contiguous
+    return part.owners
+
+
+def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, case="small"):
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -668,15 +735,9 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False):
     pkg = dlrm_pkg.load()
     from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
     dev = torch.device("cuda:0")
-    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 64, 2
+    rows, D, B, L, tabs, idx, x, dout = _shard_inputs(case, world)
     T, Bg = len(rows), B * world
-    rng = np.random.default_rng(7)
-    tabs = rand_tables(rng, rows, D)
-    idx = rand_indices(rng, rows, Bg, L)
-    x = rng.standard_normal((Bg, D)).astype(np.float32)
-    F = T + 1
-    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
-    part = TablePartition(T, world, owners)
+    part = TablePartition(T, world, _shard_owners(case, owners, world))
     mine = part.tables(rank)
     ops = HipShardOps([torch.from_numpy(tabs[t]).to(dev) for t in mine], Bg, L, 0.25, device=dev)
     eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, dev)
@@ -696,11 +757,14 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("owners,graphed", [(None, False), ([[4, 0, 2], [1, 3]], True)])
-def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed):
-    """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange; contiguous
-    or byte-balanced table assignment; eager or hipGraph-segment launches) equals the
-    single-GPU HotPath on the global batch bit for bit."""
+@pytest.mark.parametrize("owners,graphed,case", [(None, False, "small"), ([[4, 0, 2], [1, 3]], True, "small"),
+                                                 ("fitting", True, "terabyte-scaled")])
+def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed, case):
+    """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange; contiguous,
+    explicit or TablePartition.fitting's byte-balanced non-contiguous assignment; eager or
+    hipGraph-segment launches) equals the single-GPU HotPath on the global batch bit for bit.
+    "terabyte-scaled": configs[3]'s row counts (scaled), Zipf hot rows, the partition the
+    Terabyte tables need at 2 GPUs."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -708,21 +772,15 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, gra
     port = s.getsockname()[1]
     s.close()
     world = 2
-    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path), owners, graphed), nprocs=world,
+    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path), owners, graphed, case), nprocs=world,
                        start_method="spawn")
-    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 64, 2
+    rows, D, B, L, tabs, idx, x, dout = _shard_inputs(case, world)
     T, Bg = len(rows), B * world
-    rng = np.random.default_rng(7)
-    tabs = rand_tables(rng, rows, D)
-    idx = rand_indices(rng, rows, Bg, L)
-    x = rng.standard_normal((Bg, D)).astype(np.float32)
-    F = T + 1
-    dout = rng.standard_normal((Bg, D + F * (F - 1) // 2)).astype(np.float32)
     hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), Bg, L, lr=0.25, index_base=0)
     p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(T, Bg, L).to(gpu))
     hp.step(torch.from_numpy(x).to(gpu), p, torch.from_numpy(dout).to(gpu))
     from dlrm_jl_amd.sharded import TablePartition
-    part = TablePartition(T, world, owners)
+    part = TablePartition(T, world, _shard_owners(case, owners, world))
     for r in range(world):
         z = np.load(tmp_path / f"g{r}.npz")
         sl = slice(r * B, (r + 1) * B)
@@ -809,3 +867,46 @@ def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype):
     assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
     for a, b in zip(hp.ts, ts2):
         assert np.array_equal(to_np_bits(a.data), to_np_bits(b.data))
+
+
+# ------------------------------------------------------------------ the C-ABI exchange (RCCL)
+def test_comm_abi_world1_exchange_and_sharded_step(pkg, gpu):
+    """dlrm_comm_unique_id / dlrm_comm_init / dlrm_alltoall_fwd / _bwd through ctypes on a one-rank
+    RCCL communicator (the 1-GPU box has no peers): the exchanges deliver their blocks bit for bit,
+    and the sharded step driven through them equals the single-GPU HotPath."""
+    from dlrm_jl_amd.comm import CommExchange
+    from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
+    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 128, 1
+    T = len(rows)
+    comm = CommExchange(0, 1, gpu)
+    send = torch.randn((T * B * D,), device=gpu).to(torch.bfloat16)
+    recv = torch.empty_like(send)
+    comm.alltoall_fwd(send, recv, D, B, [T])
+    g = torch.randn((T * B * D,), device=gpu)
+    grecv = torch.empty_like(g)
+    comm.alltoall_bwd(g, grecv, D, B, [T])
+    torch.cuda.synchronize()
+    assert torch.equal(recv, send) and torch.equal(grecv, g)
+    with pytest.raises(TypeError):  # the gradient exchange is fp32
+        comm.alltoall_bwd(g.to(torch.bfloat16), grecv, D, B, [T])
+    import ctypes
+    h = ctypes.c_void_p()
+    assert comm.lib.dlrm_comm_init(comm.ctx.bind(), comm._uid, 3, 1, ctypes.byref(h)) == pkg._lib.E_ARG  # rank 3 of 1
+    comm.close()
+    rng = np.random.default_rng(17)
+    tabs = rand_tables(rng, rows, D)
+    idx = rand_indices(rng, rows, B, L)
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu)
+    p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).reshape(T, B, L).to(gpu))
+    ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
+    eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange="abi")
+    eng.step(x, p, dout)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, L, lr=0.25, index_base=0)
+    hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    ops.ctx.check_bounds()
+    assert torch.equal(eng.out, hp.out) and torch.equal(eng.dx, hp.dx)
+    for a, b in zip(ops.ts, hp.ts):
+        assert torch.equal(a.data, b.data)
