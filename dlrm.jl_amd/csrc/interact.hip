@@ -587,6 +587,180 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
                                          dt, dt_ld, ga, x, x_ld, su);
 }
 
+// The training step's backward with each sample split over TWO waves by column halves (wave h
+// takes the 64-column super-blocks sb = h, h + 2, ...): every wave's dependent chain (indices ->
+// rows -> MFMA -> stores) is half as long and needs about half the registers, so four waves per
+// SIMD stay resident (B = 2048: all 4096 waves at once) instead of two.  The math per
+// super-block is bwd_body's MFMA sequence, so dx, dt and the tables are bit-identical to
+// interact_bwd_update_kernel's.
+// This path is bound by the vector-memory INSTRUCTION rate of a CU as much as by bytes, so a wave
+// issues few loads:
+//  - lane t < T loads table t's index and once-hit flag for the sample (one instruction each),
+//    validates it and shuffles the row to the lanes that need it (ds_bpermute, not the TA);
+//  - the packed pair gradients dout[b][d : d + P] are staged in LDS by the pair's two waves
+//    with contiguous loads, and the MFMA A operand S[i][j] is read from there by pair index (no
+//    S matrix, no scatter);
+//  - dout's x part (dx = dout_x + dt row 0) is one coalesced load of the wave's 64 columns,
+//    redistributed by shuffles;
+//  - a once-hit row's old value comes from the gathered rows, moved from the B-operand layout
+//    (lane (c, q): row 4s + q) to the accumulator layout (row 16I + 4q + r) through the wave's
+//    LDS tile, not re-read from HBM.
+// One block = two samples (grid = ceil(B / 2)), one pass: both barriers are reached by every wave.
+template <typename T, int NB, int DC>
+__global__ __launch_bounds__(256, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
+                                                                   int64_t dout_ld, float* __restrict__ dx,
+                                                                   int64_t dx_ld, float* __restrict__ dt,
+                                                                   int64_t dt_ld, GatherArgs ga,
+                                                                   const T* __restrict__ x, int64_t x_ld,
+                                                                   StepUpdate su) {
+    constexpr int NS = 16 * NB;
+    constexpr int KS = 4 * NB;
+    constexpr int PMAX = NS * (NS - 1) / 2;
+    const int d = DC > 0 ? DC : d_;
+    __shared__ float pk_all[2][PMAX];  // the pair's packed gradient row
+    __shared__ __attribute__((aligned(16))) float tt_all[4][NS * 64];  // each wave's 64-column tile of T
+    __shared__ TableDesc tds[NS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int pair = w >> 1, h = w & 1;
+    const int c = lane & 15, q = lane >> 4;
+    const int64_t b = (int64_t)blockIdx.x * 2 + pair;
+    const bool live = b < B;
+    const int64_t bb = live ? b : 0;  // a padding sample reads sample 0 (and stores nothing)
+    const int ksteps = (F + 3) / 4;
+    const int P = F * (F - 1) / 2;
+    const T* ob = dout + bb * dout_ld;
+    float* pk = pk_all[pair];
+    float* Tt = tt_all[w];
+    if (h == 0) WT(1, 0, b);
+    for (int t = threadIdx.x; t < F - 1; t += blockDim.x) tds[t] = load_table(ga.tabs, t);
+    // ---- every independent load first: table `lane`'s index and flag, the packed gradients, x part
+    const bool tl = lane < F - 1;
+    const int64_t myidx = load_index_if(tl, ga.idx, ga.itype, (int64_t)(tl ? lane : 0) * ga.tstride + bb);
+    const uint8_t myfl = ldg<uint8_t>(su.single + (tl ? (int64_t)lane * su.cap + bb : 0));
+    float pv[(PMAX + 127) / 128];
+#pragma unroll
+    for (int k = 0; k < (PMAX + 127) / 128; ++k) {
+        const int p = h * 64 + lane + 128 * k;
+        const float v = to_f32(ldg<T>(ob + d + (p < P ? p : 0)));
+        pv[k] = p < P ? v : 0.0f;
+    }
+    float xv[DC > 0 ? (DC / 64 + 1) / 2 : 4];
+    constexpr int SBW = DC > 0 ? (DC / 64 + 1) / 2 : 4;  // super-blocks per wave (d <= 512 when not fixed)
+#pragma unroll
+    for (int sbi = 0; sbi < SBW; ++sbi) {
+        const int n = 64 * h + 128 * sbi + lane;
+        xv[sbi] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
+    }
+    const bool frozen = *su.err != 0;  // a bounds error this step: no table row is written
+#pragma unroll
+    for (int k = 0; k < (PMAX + 127) / 128; ++k) {
+        const int p = h * 64 + lane + 128 * k;
+        if (p < PMAX) pk[p] = pv[k];
+    }
+    __syncthreads();  // tds, pk
+    // validate this lane's table index; rows travel as 32-bit (~0u = invalid / no table)
+    uint32_t myrow = ~0u;
+    if (tl) {
+        const int64_t r = myidx - ga.base;
+        if (r >= 0 && r < tds[lane].nrows) myrow = (uint32_t)r;
+        else if (h == 0 && live) raise_index_error(ga.err);
+    }
+    const T* rowp[KS];
+    unsigned livek = 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int kk = 4 * s + q;
+        const uint32_t r = (uint32_t)__shfl((int)myrow, kk >= 1 ? kk - 1 : 0, 64);
+        const bool tab = s < ksteps && kk >= 1 && kk < F && r != ~0u;
+        const T* src = (s < ksteps && kk == 0) ? x + bb * x_ld
+                                               : (tab ? (const T*)tds[kk - 1].data + (int64_t)r * d : nullptr);
+        livek |= src ? (1u << s) : 0u;
+        rowp[s] = src ? src : ob;
+    }
+    uint32_t urow[NB][4];
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = I * 16 + 4 * q + r;
+            const int src = (f >= 1 && f < F) ? f - 1 : 0;
+            const uint32_t row = (uint32_t)__shfl((int)myrow, src, 64);
+            const int fl = __shfl((int)myfl, src, 64);
+            urow[I][r] = (f >= 1 && f < F && !frozen && fl != 0) ? row : ~0u;
+        }
+    if (h == 0) WT(1, 1, b);
+#pragma unroll
+    for (int sbi = 0; sbi < SBW; ++sbi) {
+        const int sb = 64 * h + 128 * sbi;
+        if (sb >= d) break;
+        const int n0 = sb + 4 * c;  // this lane's 4 output columns
+        const bool colok = n0 < d;
+        const int nc = colok ? n0 : 0;
+        f32x4_t bv[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const f32x4_t v = load4_f32(rowp[s] + nc);
+            bv[s] = ((livek >> s) & 1u) && colok ? v : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+        if (sbi > 0) wave_lds_sync();  // the previous super-block's tile reads are done
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            if (s < ksteps) *(f32x4_t*)(Tt + (4 * s + q) * 64 + 4 * c) = bv[s];
+        f32x4_t acc[NB][4];
+#pragma unroll
+        for (int I = 0; I < NB; ++I)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s < ksteps) {
+                const int kk = 4 * s + q;
+#pragma unroll
+                for (int I = 0; I < NB; ++I) {
+                    // S[16I+c][kk]: the symmetric zero-diagonal unpack of the pair row
+                    const int i = I * 16 + c;
+                    const int hi = i > kk ? i : kk, lo = i > kk ? kk : i;
+                    const float av = (i != kk && hi < F) ? pk[hi * (hi - 1) / 2 + lo] : 0.0f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s][e], acc[I][e], 0, 0, 0);
+                }
+            }
+        }
+        if (h == 0 && sbi == 0) WT(1, 2, b);
+        // dout's x part for this lane's columns (lanes 0..15 hold output row 0)
+        f32x4_t xo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xo[e] = __shfl(xv[sbi], 4 * c + e, 64);
+        wave_lds_sync();  // the tile of T (written before the MFMAs)
+        if (!live || !colok) continue;
+#pragma unroll
+        for (int I = 0; I < NB; ++I)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = I * 16 + 4 * q + r;
+                if (f < F) {
+                    const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
+                    if (urow[I][r] != ~0u) {
+                        float wv[4];
+                        const f32x4_t tw = *(const f32x4_t*)(Tt + f * 64 + 4 * c);  // the row as gathered
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
+                        store_row<T, 4>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
+                    } else {
+                        stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+                    }
+                    if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo + v);
+                }
+            }
+        if (h == 0 && sbi == 0) {
+            WT(1, 3, b);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            WT(1, 4, b);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ scalar fallbacks
 template <typename T>
 __global__ __launch_bounds__(256) void interact_fwd_scalar(int d, int F, int B, const T* __restrict__ x, int64_t x_ld,
@@ -905,6 +1079,29 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     StepUpdate su{ix.single, ix.cap, lr, ctx_error_word(ctx)};
     // one super-block of T rows in flight: two (the gather backward's choice) spill here
     static const int sbu = getenv("DLRM_UPD_SBU") ? atoi(getenv("DLRM_UPD_SBU")) : 1;  // experiment knob
+    // d = 128 (>= two 64-column super-blocks): two waves per sample (interact_bwd_split_kernel)
+    static const bool split = !getenv("DLRM_BWD_SPLIT") || atoi(getenv("DLRM_BWD_SPLIT")) != 0;
+    if (split && d == 128) {
+        const dim3 grid((unsigned)((B + 1) / 2)), blk(256);
+        if (dtype == DLRM_F32) {
+            if (NB == 1)
+                hipLaunchKernelGGL((interact_bwd_split_kernel<float, 1, 128>), grid, blk, 0, s, d, F, B,
+                                   (const float*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const float*)x, x_ld, su);
+            else
+                hipLaunchKernelGGL((interact_bwd_split_kernel<float, 2, 128>), grid, blk, 0, s, d, F, B,
+                                   (const float*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const float*)x, x_ld, su);
+        } else {
+            if (NB == 1)
+                hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, 1, 128>), grid, blk, 0, s, d, F, B,
+                                   (const uint16_t*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const uint16_t*)x, x_ld,
+                                   su);
+            else
+                hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, 2, 128>), grid, blk, 0, s, d, F, B,
+                                   (const uint16_t*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const uint16_t*)x, x_ld,
+                                   su);
+        }
+        return ctx_hip(ctx, hipGetLastError(), "step_bwd(split) launch");
+    }
 #define DLRM_LAUNCH_BWDUP(TY, N_)                                                                                  \
     {                                                                                                              \
         typedef BwdGeom<N_> G;                                                                                     \

@@ -53,6 +53,8 @@ for mode in sys.argv[1:] or ["ops"]:
         print("bwd_gather (no indexer):")
         hp.interact_bwd(dout, x=x, idx=packs[1]); torch.cuda.synchronize()
         show(1, 5, ["start", "S built", "sb0 mfma", "sb1 mfma", "stores"])
+        if os.environ.get("DLRM_BWD_SPLIT", "1") != "0":
+            print("  (split backward: slots = start, S barrier, MFMA done, stores issued, stores drained)")
     else:
         print("step_fwd:")
         hp.step_fwd(x, packs[2]); torch.cuda.synchronize()
@@ -60,3 +62,5 @@ for mode in sys.argv[1:] or ["ops"]:
         print("step_bwd (BWD_ONLY):")
         hp.step_bwd(dout, x=x, idx=packs[2], flags=pkg._lib.STEP_BWD_ONLY); torch.cuda.synchronize()
         show(1, 5, ["start", "S built", "sb0 mfma", "sb1 mfma", "stores"])
+        if os.environ.get("DLRM_BWD_SPLIT", "1") != "0":
+            print("  (split backward: slots = start, S barrier, MFMA done, stores issued, stores drained)")
