@@ -605,9 +605,10 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
 //  - a once-hit row's old value comes from the gathered rows, moved from the B-operand layout
 //    (lane (c, q): row 4s + q) to the accumulator layout (row 16I + 4q + r) through the wave's
 //    LDS tile, not re-read from HBM.
-// One block = two samples (grid = ceil(B / 2)), one pass: both barriers are reached by every wave.
-template <typename T, int NB, int DC>
-__global__ __launch_bounds__(256, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
+// One block = SPB samples (2·SPB waves; grid = ceil(B / SPB)), one pass: both barriers are
+// reached by every wave.  Larger blocks shorten the dispatch ramp (fewer workgroups to place).
+template <typename T, int NB, int DC, int SPB>
+__global__ __launch_bounds__(128 * SPB, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
                                                                    int64_t dout_ld, float* __restrict__ dx,
                                                                    int64_t dx_ld, float* __restrict__ dt,
                                                                    int64_t dt_ld, GatherArgs ga,
@@ -617,13 +618,13 @@ __global__ __launch_bounds__(256, 4) void interact_bwd_split_kernel(int d_, int 
     constexpr int KS = 4 * NB;
     constexpr int PMAX = NS * (NS - 1) / 2;
     const int d = DC > 0 ? DC : d_;
-    __shared__ float pk_all[2][PMAX];  // the pair's packed gradient row
-    __shared__ __attribute__((aligned(16))) float tt_all[4][NS * 64];  // each wave's 64-column tile of T
+    __shared__ float pk_all[SPB][PMAX];  // each sample's packed gradient row
+    __shared__ __attribute__((aligned(16))) float tt_all[2 * SPB][NS * 64];  // each wave's 64-column tile of T
     __shared__ TableDesc tds[NS];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pair = w >> 1, h = w & 1;
     const int c = lane & 15, q = lane >> 4;
-    const int64_t b = (int64_t)blockIdx.x * 2 + pair;
+    const int64_t b = (int64_t)blockIdx.x * SPB + pair;
     const bool live = b < B;
     const int64_t bb = live ? b : 0;  // a padding sample reads sample 0 (and stores nothing)
     const int ksteps = (F + 3) / 4;
@@ -1082,24 +1083,27 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     // d = 128 (>= two 64-column super-blocks): two waves per sample (interact_bwd_split_kernel)
     static const bool split = !getenv("DLRM_BWD_SPLIT") || atoi(getenv("DLRM_BWD_SPLIT")) != 0;
     if (split && d == 128) {
-        const dim3 grid((unsigned)((B + 1) / 2)), blk(256);
+        // samples per block (DLRM_BWD_SPB = 2, 4 or 8 overrides)
+        static const int spb = [] {
+            const char* e = getenv("DLRM_BWD_SPB");
+            const int v = e ? atoi(e) : 4;
+            return v >= 8 ? 8 : (v >= 4 ? 4 : 2);
+        }();
+#define DLRM_LAUNCH_SPLIT(TY, N_, S_)                                                                              \
+    hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 128, S_>), dim3((unsigned)((B + S_ - 1) / S_)),            \
+                       dim3(128 * S_), 0, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x,  \
+                       x_ld, su)
+#define DLRM_LAUNCH_SPLIT_S(TY, N_)                 \
+    if (spb == 8) DLRM_LAUNCH_SPLIT(TY, N_, 8);     \
+    else if (spb == 4) DLRM_LAUNCH_SPLIT(TY, N_, 4); \
+    else DLRM_LAUNCH_SPLIT(TY, N_, 2);
         if (dtype == DLRM_F32) {
-            if (NB == 1)
-                hipLaunchKernelGGL((interact_bwd_split_kernel<float, 1, 128>), grid, blk, 0, s, d, F, B,
-                                   (const float*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const float*)x, x_ld, su);
-            else
-                hipLaunchKernelGGL((interact_bwd_split_kernel<float, 2, 128>), grid, blk, 0, s, d, F, B,
-                                   (const float*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const float*)x, x_ld, su);
+            if (NB == 1) { DLRM_LAUNCH_SPLIT_S(float, 1) } else { DLRM_LAUNCH_SPLIT_S(float, 2) }
         } else {
-            if (NB == 1)
-                hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, 1, 128>), grid, blk, 0, s, d, F, B,
-                                   (const uint16_t*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const uint16_t*)x, x_ld,
-                                   su);
-            else
-                hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, 2, 128>), grid, blk, 0, s, d, F, B,
-                                   (const uint16_t*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const uint16_t*)x, x_ld,
-                                   su);
+            if (NB == 1) { DLRM_LAUNCH_SPLIT_S(uint16_t, 1) } else { DLRM_LAUNCH_SPLIT_S(uint16_t, 2) }
         }
+#undef DLRM_LAUNCH_SPLIT_S
+#undef DLRM_LAUNCH_SPLIT
         return ctx_hip(ctx, hipGetLastError(), "step_bwd(split) launch");
     }
 #define DLRM_LAUNCH_BWDUP(TY, N_)                                                                                  \
