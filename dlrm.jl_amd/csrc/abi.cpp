@@ -512,8 +512,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     Piece pieces[] = {
         {(void**)&ix->dev.keys0, n0 * 4},    {(void**)&ix->dev.keys1, n0 * 4},  {(void**)&ix->dev.vals0, n0 * 4},
         {(void**)&ix->dev.vals1, n0 * 4},    {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
-        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 16}, {(void**)&ix->dev.hot, n * 16},
-        {(void**)&ix->dev.hot_slice, n * 4}, {(void**)&ix->dev.hot_cnt, n * 4},
+        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 32}, {(void**)&ix->dev.hot, n * 16},
+        {(void**)&ix->dev.hot_slice, n * 16}, {(void**)&ix->dev.hot_cnt, n * 4},
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)

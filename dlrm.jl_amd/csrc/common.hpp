@@ -167,9 +167,9 @@ struct IndexerDev {
     int32_t* perm;         // positions grouped by row, ascending within a row
     int32_t* seg_start;    // [cap+1]
     uint32_t* seg_row;
-    int4* chunks;          // segments of <= kChunk positions: {beg, end, row, first position}
+    int4* chunks;          // [2 cap] per table: segments of <= kChunk positions (indexer.hpp write_chunk)
     int4* hot;             // longer segments: {beg, end, row, first slice}
-    int32_t* hot_slice;    // slice -> its hot segment (slices of kHotSlice positions)
+    int4* hot_slice;       // their slices of kHotSlice positions: {p0, p1, row, hot segment}
     int32_t* hot_cnt;      // arrivals per hot segment (multi-slice combine; reset by the last)
     float* partial;        // [T][pcap][pdim] slice partial sums (multi-slice hot segments)
     int32_t* counts;       // [T][8]: U, chunks, hot, slices, nvalid

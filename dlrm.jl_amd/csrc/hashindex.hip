@@ -194,12 +194,13 @@ __global__ __launch_bounds__(256) void hix_alloc_kernel(IndexerDev ix, int split
         ix.hfill[ho + s0 + q] = 0;
         ix.seg_start[(int64_t)t * (ix.cap + 1) + seg] = beg;
         ix.seg_row[off + seg] = row[q];
-        if (chunk) ix.chunks[off + (int)sbase[1] + (int)(bex & M21)] = make_int4(beg, end, (int)row[q], -1);
+        // (a chunk's inline positions are written by the order pass, once they are sorted)
+        if (chunk) write_chunk(ix.chunks + 2 * off, (int)sbase[1] + (int)(bex & M21), beg, end, (int)row[q], nullptr);
         if (hot) {
             const int h = (int)sbase[2] + (int)((bex >> 21) & M21);
             const int sl0 = (int)sbase[3] + (int)((bex >> 42) & M21);
             ix.hot[off + h] = make_int4(beg, end, (int)row[q], sl0);
-            for (int k = 0; k < ns; ++k) ix.hot_slice[off + sl0 + k] = h;
+            write_slices(ix.hot_slice + off, sl0, beg, end, (int)row[q], h);
         }
         aex += (1ll << 32) | c[q];
         bex += (chunk ? 1ll : 0ll) | ((hot ? 1ll : 0ll) << 21) | ((long long)ns << 42);
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(256) void hix_order_kernel(IndexerDev ix, int T_, i
             int4 cd[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
-                cd[u] = tc[u] >= 0 ? ix.chunks[(int64_t)tc[u] * ix.cap + cl[u]] : make_int4(0, 0, 0, 0);
+                cd[u] = tc[u] >= 0 ? ix.chunks[2 * ((int64_t)tc[u] * ix.cap + cl[u])] : make_int4(0, 0, 0, 0);
             int v[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256) void hix_order_kernel(IndexerDev ix, int T_, i
                 if (hl < len) {
                     const int64_t off = (int64_t)tc[u] * ix.cap;
                     ix.perm[off + cd[u].x + rank] = v[u];
-                    if (rank == 0) ix.chunks[off + cl[u]].w = v[u];
+                    if (rank < kChunkInline) ((int*)(ix.chunks + 2 * (off + cl[u])))[3 + rank] = v[u];
                 }
             }
             continue;

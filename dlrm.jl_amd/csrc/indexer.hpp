@@ -13,9 +13,29 @@ namespace dlrm {
 constexpr int kChunk = 32;          // max positions of a segment handled by one lane group
 constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
 enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
-// Hot segments are cut into slices of kHotSlice positions, one work item each; a segment of
-// several slices is combined by its last-arriving slice (sc1 partial rows + a counter).
+// Hot segments are cut into slices of kHotSlice positions, one work item (one 256-thread apply
+// workgroup: 8 lane groups x 16 rows in flight at D = 128) each, so a hot row's grad rows are read
+// by several CUs at once; a segment of several slices is combined by its last-arriving slice (sc1
+// partial rows + a counter; apply.hpp).
 constexpr int kHotSlice = 128;
+// A chunk's descriptor is two int4: {beg, end, row, pos0}, {pos1, pos2, pos3, pos4}: its first
+// kChunkInline positions (ascending; -1 past the end) travel with it, so the apply reads perm
+// only for longer chunks.  A hot slice's descriptor is one int4 {p0, p1, row, hot segment}.
+constexpr int kChunkInline = 5;
+
+__device__ __forceinline__ void write_chunk(int4* chunks, int64_t c, int beg, int end, int row,
+                                            const int32_t* sorted_pos /* [beg, end) or NULL */) {
+    int q[kChunkInline];
+#pragma unroll
+    for (int k = 0; k < kChunkInline; ++k) q[k] = (sorted_pos && beg + k < end) ? sorted_pos[beg + k] : -1;
+    chunks[2 * c] = make_int4(beg, end, row, q[0]);
+    chunks[2 * c + 1] = make_int4(q[1], q[2], q[3], q[4]);
+}
+
+__device__ __forceinline__ void write_slices(int4* hot_slice, int s0, int beg, int end, int row, int h) {
+    for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice)
+        hot_slice[s0 + k] = make_int4(p0, min(p0 + kHotSlice, end), row, h);
+}
 
 // Exclusive scan over the NW waves' 64*NW threads; returns this thread's prefix, total in *tot.
 template <int NW, typename V>
@@ -410,9 +430,9 @@ __device__ void fast_index_table(const IndexerDev& ix, int v, int t, int vs, uin
     long long tot64;
     const long long ex = block_scan_nw<NT / 64, long long>(cw, sl.wtot64, &tot64);
     int c = (int)(ex & M21), hh = (int)((ex >> 21) & M21), ss = (int)((ex >> 42) & M21);
-    int4* chunks = ix.chunks + off;
+    int4* chunks = ix.chunks + 2 * off;
     int4* hot = ix.hot + off;
-    int32_t* hot_slice = ix.hot_slice + off;
+    int4* hot_slice = ix.hot_slice + off;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
         const int sidx = E * tid + q;
@@ -421,11 +441,11 @@ __device__ void fast_index_table(const IndexerDev& ix, int v, int t, int vs, uin
             if (SPLIT && len == 1) {
                 // updated by the backward (single[] flag)
             } else if (len <= kChunk) {
-                chunks[c++] = make_int4(beg[q], end[q], (int)srow[sidx], Vs[beg[q]]);
+                write_chunk(chunks, c++, beg[q], end[q], (int)srow[sidx], Vs);
             } else {
                 const int ns = (len + kHotSlice - 1) / kHotSlice;
                 hot[hh] = make_int4(beg[q], end[q], (int)srow[sidx], ss);
-                for (int k = 0; k < ns; ++k) hot_slice[ss + k] = hh;
+                write_slices(hot_slice, ss, beg[q], end[q], (int)srow[sidx], hh);
                 ++hh;
                 ss += ns;
             }

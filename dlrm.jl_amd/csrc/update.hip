@@ -56,7 +56,7 @@ extern "C" int dlrm_debug_apply_reset(void) {
 #define APPLY_END() do {} while (0)
 #endif
 
-#include "indexer.hpp"
+#include "apply.hpp"
 
 namespace dlrm {
 
@@ -192,9 +192,9 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
     PHASE(20);
     const int nvalid = sl.nvalid;
     if (tid == 0) seg_start[U] = nvalid;
-    int4* chunks = ix.chunks + off;
+    int4* chunks = ix.chunks + 2 * off;
     int4* hot = ix.hot + off;
-    int32_t* hot_slice = ix.hot_slice + off;
+    int4* hot_slice = ix.hot_slice + off;
     long long C = 0, H = 0, S = 0;
     for (int tile = 0; tile < U; tile += kBuildThreads) {
         const int s = tile + tid;
@@ -209,12 +209,12 @@ __device__ void build_segments(const IndexerDev& ix, int t, const uint32_t* K, c
         long long tot, tots;
         const long long ex = block_scan_excl<long long>((isc ? 1ll : 0ll) | ((ish ? 1ll : 0ll) << 32), sl.wtot64, &tot);
         const long long exs = block_scan_excl<long long>((long long)ns, sl.wtot64, &tots);
-        if (isc) chunks[C + (ex & 0xffffffffll)] = make_int4(beg, end, (int)srow[s], V[beg]);
+        if (isc) write_chunk(chunks, C + (ex & 0xffffffffll), beg, end, (int)srow[s], V);
         if (ish) {
             const int h = (int)(H + (ex >> 32));
             const int s0 = (int)(S + exs);
             hot[h] = make_int4(beg, end, (int)srow[s], s0);
-            for (int k = 0; k < ns; ++k) hot_slice[s0 + k] = h;
+            write_slices(hot_slice, s0, beg, end, (int)srow[s], h);
         }
         C += tot & 0xffffffffll;
         H += tot >> 32;
@@ -325,146 +325,21 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 }
 
 // ------------------------------------------------------------------------------ apply
-// Lane-group geometry: D elements = VPR vectors of 16 B of the GRAD dtype; a group of LPR
-// lanes owns one row, a wave holds RPW groups.
-template <typename GT, int VPR>
-struct ApplyGeom {
-    typedef Vec<GT> GV;
-    static constexpr int NE = GV::N;
-    static constexpr int D = VPR * NE;
-    static constexpr int LPR = VPR <= 64 ? VPR : 64;
-    static constexpr int VPL = VPR <= 64 ? 1 : VPR / 64;
-    static constexpr int RPW = 64 / LPR;
-};
-
-// Sums the grad rows of positions [beg, end) in ascending order into acc (8 rows in flight).
-// first >= 0 is perm[beg] when the caller already has it (saves one dependent load).
-template <typename GT, int VPR>
-__device__ __forceinline__ void sum_positions(const int32_t* __restrict__ perm, int beg, int end, int L,
-                                              const GT* __restrict__ gbase, int64_t grad_ld, int v,
-                                              float (&acc)[ApplyGeom<GT, VPR>::VPL][ApplyGeom<GT, VPR>::NE],
-                                              int first = -1) {
-    typedef ApplyGeom<GT, VPR> G;
-    typedef typename G::GV GV;
-    constexpr int U = 8;
-    for (int i = beg; i < end; i += U) {
-        int32_t p[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            p[u] = (u == 0 && i == beg && first >= 0) ? first : ((i + u < end) ? perm[i + u] : -1);
-        typename GV::type gv[U][G::VPL];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (p[u] >= 0) {
-                const GT* gr = gbase + (int64_t)(p[u] / L) * grad_ld;
-#pragma unroll
-                for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
-            }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (p[u] >= 0) {
-#pragma unroll
-                for (int j = 0; j < G::VPL; ++j) {
-                    float f[G::NE];
-                    GV::to_f32(gv[u][j], f);
-#pragma unroll
-                    for (int e = 0; e < G::NE; ++e) acc[j][e] += f[e];
-                }
-            }
-    }
-}
-
-// grid.x = chunk blocks + hot blocks, grid.y = tables.  Chunk blocks: one lane group per
-// chunk, no loop (the grid covers the worst case; idle groups exit).  Hot blocks: one
-// workgroup per hot segment; lane groups sum sub-chunks of `cs` positions into LDS, then
-// the partials are added in sub-chunk order and the row is written once.
-// Hot segments: the 4*RPW lane groups of the workgroup take contiguous equal slices (size set
-// by the segment length only); each stages its slice's positions in LDS with one cooperative
-// read, then sums the grad rows in position order with kHotInFlight rows in flight.  The
-// group partials are added in group order and the row is written once.
-constexpr int kHotInFlight = 8;   // grad rows in flight per lane group
-
-template <typename GT, int VPR>
-__device__ __forceinline__ void sum_staged(const int32_t* stage, int m, int L, const GT* __restrict__ gbase,
-                                           int64_t grad_ld, int v,
-                                           float (&acc)[ApplyGeom<GT, VPR>::VPL][ApplyGeom<GT, VPR>::NE]) {
-    typedef ApplyGeom<GT, VPR> G;
-    typedef typename G::GV GV;
-    constexpr int IF = kHotInFlight / G::VPL;  // rows in flight (16-B vectors per lane bounded)
-    for (int i = 0; i < m; i += IF) {
-        typename GV::type gv[IF][G::VPL];
-#pragma unroll
-        for (int u = 0; u < IF; ++u)
-            if (i + u < m) {
-                const GT* gr = gbase + (int64_t)(stage[i + u] / L) * grad_ld;
-#pragma unroll
-                for (int j = 0; j < G::VPL; ++j) gv[u][j] = *((const typename GV::type*)gr + v + j * 64);
-            }
-#pragma unroll
-        for (int u = 0; u < IF; ++u)
-            if (i + u < m) {
-#pragma unroll
-                for (int j = 0; j < G::VPL; ++j) {
-                    float f[G::NE];
-                    GV::to_f32(gv[u][j], f);
-#pragma unroll
-                    for (int e = 0; e < G::NE; ++e) acc[j][e] += f[e];
-                }
-            }
-    }
-}
-
-// Cross-workgroup hand-off of slice partials (cdna_hip_programming.md Guideline 16, R1):
-// payload stored write-through (sc1, agent-scope atomic stores), every storing wave drains
-// (vmcnt(0)) before the workgroup barrier, ONE lane adds to the segment's arrival counter;
-// the last arriver reads every partial with sc1 loads (no acquire needed) and resets the
-// counter for the next launch.
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) int gi32_t;
-
-__device__ __forceinline__ void store_sc1(float* p, const f32x4& v) {
-    const unsigned long long lo = ((unsigned long long)__float_as_uint(v[1]) << 32) | __float_as_uint(v[0]);
-    const unsigned long long hi = ((unsigned long long)__float_as_uint(v[3]) << 32) | __float_as_uint(v[2]);
-    __hip_atomic_store((gu64_t*)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu64_t*)(p + 2), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ f32x4 load_sc1(const float* p) {
-    const unsigned long long lo = __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long hi = __hip_atomic_load((gu64_t*)(p + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return f32x4{__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)), __uint_as_float((uint32_t)hi),
-                 __uint_as_float((uint32_t)(hi >> 32))};
-}
-
-template <typename TT>
-__device__ __forceinline__ void sgd_row4(TT* row, int c0, const f32x4& sum, float lr) {
-    float f[4];
-    load_row<TT, 4>(row, c0, f);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) f[e] = __builtin_fmaf(-lr, sum[e], f[e]);
-    store_row<TT, 4>(row, c0, f);
-}
-
-// Persistent launch, flat over tables.  Work items: [0, S) = the S slices of every table's hot
-// segments (kHotSlice positions, one workgroup each, handed out first), then ceil(C / NG)
-// items of NG chunks (one per lane group).  Workgroup b takes items b, b + grid, ...: every
-// item is short, so static striding balances, and no workgroup is launched past the work.
-template <typename TT, typename GT, int VPR, int CPG>
-__global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_, int L,
-                                                        const GT* __restrict__ grad, int64_t grad_ld,
-                                                        int64_t grad_offset, float lr,
-                                                        const unsigned* __restrict__ err) {
+// Persistent launch, flat over tables (apply.hpp).  Work items: [0, S) = the S slices of every
+// table's hot segments (one workgroup each, handed out first: the longest chains), then
+// ceil(C / NG) items of NG chunks (one per lane group).  Workgroup b takes items b, b + grid, ...:
+// every item is short, so static striding balances, and no workgroup is launched past the work.
+template <typename TT, typename GT, int VPR>
+__global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_,
+                                                                  int L, const GT* __restrict__ grad, int64_t grad_ld,
+                                                                  int64_t grad_offset, float lr,
+                                                                  const unsigned* __restrict__ err) {
     // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
     // this step): the reference's gather throws before update!, so no table row is written
     if (*err) return;
     typedef ApplyGeom<GT, VPR> G;
-    constexpr int NE = G::NE;
-    constexpr int D = G::D;
-    constexpr int NG = 4 * G::RPW;                      // lane groups per workgroup
-    constexpr int PER = (kHotSlice + NG - 1) / NG;       // positions of a slice per lane group
-    __shared__ __attribute__((aligned(16))) float hot_part[NG][D];  // <= 8 KB
-    __shared__ int32_t hot_stage[NG][PER];
-    __shared__ int sh_last;
+    constexpr int D = G::D, NG = G::NG;
+    __shared__ SliceLds<D> sm;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane / G::LPR, v = lane % G::LPR;
     const int gid = w * G::RPW + g;
@@ -474,88 +349,23 @@ __global__ __launch_bounds__(256) void sgd_apply_kernel(IndexerDev ix, TableDesc
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
         APPLY_START(item >= sS.total ? 1 : 2);
         if (item >= sS.total) {
-            // ---- NG chunks: one per lane group (table row prefetched while the grad rows of
-            // its positions stream in, summed in ascending position order)
             int tc, cl;
             locate(ix, T_, CNT_C, sC, (item - sS.total) * NG + gid, tc, cl);
             if (g >= G::RPW || tc < 0) continue;
-            const int64_t off = (int64_t)tc * ix.cap;
-            const GT* gbase = grad + grad_offset + (int64_t)(tc >> ix.vshift) * D;
-            const int4 cd = ix.chunks[off + cl];
-            TT* row = (TT*)tabs[tc >> ix.vshift].data + (int64_t)(uint32_t)cd.z * D;
-            float tv[G::VPL][NE];
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j) load_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
-            float acc[G::VPL][NE];
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j)
-#pragma unroll
-                for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-            sum_positions<GT, VPR>(ix.perm + off, cd.x, cd.y, L, gbase, grad_ld, v, acc, cd.w);
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j) {
-#pragma unroll
-                for (int e = 0; e < NE; ++e) tv[j][e] = __builtin_fmaf(-lr, acc[j][e], tv[j][e]);
-                store_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
-            }
+            const int64_t co = 2 * ((int64_t)tc * ix.cap + cl);
+            const int4 ca = ix.chunks[co], cb = ix.chunks[co + 1];
+            const int t = tc >> ix.vshift;
+            run_chunk<TT, GT, VPR>(ix.perm + (int64_t)tc * ix.cap, ca, cb, (TT*)tabs[t].data,
+                                   grad + grad_offset + (int64_t)t * D, grad_ld, L, lr, v, lane - v);
             APPLY_END();
             continue;
         }
-        // ---- one slice of a hot segment: lane groups sum contiguous parts, in group order
         int th, sl;
         locate(ix, T_, CNT_S, sS, item, th, sl);  // item < S: found, the same for every lane
-        const int64_t off = (int64_t)th * ix.cap;
-        const int hseg = ix.hot_slice[off + sl];
-        const int4 hd = ix.hot[off + hseg];
-        const int ns = (hd.y - hd.x + kHotSlice - 1) / kHotSlice;
-        const int p0 = hd.x + (sl - hd.w) * kHotSlice, p1 = min(p0 + kHotSlice, hd.y);
-        {
-            float acc[G::VPL][NE];
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j)
-#pragma unroll
-                for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-            const int b0 = min(p0 + gid * PER, p1), m = min(b0 + PER, p1) - b0;
-            const int32_t* perm = ix.perm + off;
-            int32_t* stage = hot_stage[gid];
-            for (int k = v; k < m; k += G::LPR) stage[k] = perm[b0 + k];
-            wave_lds_sync();
-            sum_staged<GT, VPR>(stage, m, L, grad + grad_offset + (int64_t)(th >> ix.vshift) * D, grad_ld, v, acc);
-#pragma unroll
-            for (int j = 0; j < G::VPL; ++j)
-#pragma unroll
-                for (int e = 0; e < NE; e += 4)
-                    *(f32x4*)(&hot_part[gid][(v + j * 64) * NE + e]) =
-                        f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
-        }
-        __syncthreads();
-        TT* row = (TT*)tabs[th >> ix.vshift].data + (int64_t)(uint32_t)hd.z * D;
-        float* part = ix.partial + ((int64_t)th * ix.pcap + sl) * ix.pdim;
-        for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
-            f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int c = 0; c < NG; ++c) sum += *(const f32x4*)(&hot_part[c][c0]);
-            if (ns == 1) sgd_row4<TT>(row, c0, sum, lr);
-            else store_sc1(part + c0, sum);
-        }
-        if (ns > 1) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-            __syncthreads();
-            if (threadIdx.x == 0)
-                sh_last = __hip_atomic_fetch_add((gi32_t*)(ix.hot_cnt + off + hseg), 1, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
-            __syncthreads();
-            if (sh_last) {
-                const float* first = ix.partial + ((int64_t)th * ix.pcap + hd.w) * ix.pdim;
-                for (int c0 = threadIdx.x * 4; c0 < D; c0 += blockDim.x * 4) {
-                    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-                    for (int k = 0; k < ns; ++k) sum += load_sc1(first + (int64_t)k * ix.pdim + c0);
-                    sgd_row4<TT>(row, c0, sum, lr);
-                }
-                if (threadIdx.x == 0)
-                    __hip_atomic_store((gi32_t*)(ix.hot_cnt + off + hseg), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        __syncthreads();  // hot_part / hot_stage / sh_last reused by this workgroup's next item
+        const int4 sd = ix.hot_slice[(int64_t)th * ix.cap + sl];
+        const int t = th >> ix.vshift;
+        run_slice<TT, GT, VPR>(ix, th, sl, sd, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, L, lr,
+                               sm);
         APPLY_END();
     }
 }
@@ -573,7 +383,7 @@ __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDes
     TT* table = (TT*)tabs[t >> ix.vshift].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int cid = (int)(e / D), c = (int)(e % D);
-        const int4 cd = ix.chunks[off + cid];
+        const int4 cd = ix.chunks[2 * (off + cid)];
         float acc = 0.0f;
         for (int i = cd.x; i < cd.y; ++i)
             acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)(t >> ix.vshift) * D + c]);
@@ -687,24 +497,22 @@ template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
                              int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err) {
     typedef ApplyGeom<GT, VPR> G;
-    constexpr int CPG = 1;                   // chunks per lane group (4 measured slower)
-    const int per_block = 4 * G::RPW * CPG;  // 4 waves x RPW lane groups x CPG chunks
-    // persistent grid: resident workgroups only (never more than the worst-case item count)
-    const int64_t cb = ((int64_t)T_ * N + per_block - 1) / per_block;
-    const int64_t hb = (int64_t)T_ * (N / (kChunk + 1));
+    // persistent grid: resident workgroups only (never more than the worst-case item count per
+    // table: N / kHotSlice + N / (kChunk + 1) + 1 hot slices, N / NG chunk items)
+    const int64_t ib = (int64_t)T_ * (N / kHotSlice + N / (kChunk + 1) + 1 + (N + G::NG - 1) / G::NG);
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR, CPG>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR>, kApplyThreads, 0) !=
                 hipSuccess || per_cu < 1)
-            per_cu = 4;
+            per_cu = 1;
     }
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t grid = (int64_t)per_cu * (cus > 0 ? cus : 256);
-    if (grid > cb + hb) grid = cb + hb;
-    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, CPG>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(256), 0, s,
-                       ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err);
+    if (grid > ib) grid = ib;
+    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kApplyThreads), 0,
+                       s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err);
 }
 
 template <typename TT, typename GT>
@@ -732,7 +540,7 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     const bool aligned = tabs_aligned16 && (uintptr_t)grad % 16 == 0 && (grad_ld * gesz) % 16 == 0 &&
                          (grad_offset * gesz) % 16 == 0 && (D * gesz) % 16 == 0 && (D * tesz) % 16 == 0 && D % 4 == 0;
     bool done = false;
-    const int64_t slots = (int64_t)T_ * ((N + 7) / 8 + N / (kChunk + 1));  // launch_apply_vec's grid bound
+    const int64_t slots = (int64_t)T_ * (N + 1);  // (item counts stay in int)
     if (aligned && slots < (1ll << 31)) {
         const int vpr = D * gesz / 16;
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
