@@ -103,6 +103,8 @@ SIGNATURES = {
     "dlrm_comm_destroy": (_i32, [_vp]),
     "dlrm_alltoall_fwd": (_i32, [_vp, _vp, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
     "dlrm_alltoall_bwd": (_i32, [_vp, _vp, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
+    "dlrm_interact_bwd_blocked": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp,
+                                         _i64, _vp, _vp, _vp]),
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "apply.hpp"
 
 using namespace dlrm;
 
@@ -481,6 +482,24 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer*
     return DLRM_OK;
 }
 
+int dlrm_interact_bwd_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
+                              int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld,
+                              const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dst,
+                              const int64_t* dst_base, const int64_t* dst_ld) {
+    CHECK_ARG(ctx && tb, "dlrm_interact_bwd_blocked: null ctx/tables");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    const int d = tb->D, F = tb->T + 1;
+    const int64_t P = (int64_t)F * (F - 1) / 2;
+    CHECK_ARG(padding >= 0 && x_ld >= d && dout_ld >= d + P + padding && dx_ld >= d,
+              "dlrm_interact_bwd_blocked: leading dimensions too small");
+    CHECK_ARG(batch == 0 || tb->T == 0 || (x && dout && dx && dst && dst_base && dst_ld),
+              "dlrm_interact_bwd_blocked: null buffer");
+    return launch_interact_bwd_blocked(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                       index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dst, dst_base,
+                                       dst_ld);
+}
+
 // --------------------------------------------------------------------------- indexer
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm_indexer** out) {
     CHECK_ARG(ctx && out, "dlrm_indexer_create: null argument");
@@ -565,9 +584,14 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
     CHECK_ARG((int64_t)batch * lookups <= ix->dev.cap, "dlrm_indexer_build: batch*lookups %lld > capacity %lld",
               (long long)batch * lookups, (long long)ix->dev.cap);
     ix->dev.vshift = 0;
-    rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups);
+    // the split form where the builds support it: once-hit positions flagged (single[]) instead of
+    // listed as one-position chunks; the apply then updates them with no descriptor read
+    const int64_t N = (int64_t)batch * lookups;
+    const bool split = N <= kFastMaxN || (ix->dev.hsize && N <= kHixMaxN);
+    rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups,
+                              split);
     if (rc) return rc;
-    record_build(ix, false, indices, itype, table_stride, index_base, batch, lookups);
+    record_build(ix, split, indices, itype, table_stride, index_base, batch, lookups);
     return DLRM_OK;
 }
 
@@ -687,18 +711,18 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned f
     if (flags & DLRM_UPDATE_PREBUILT) {
         if (!built_from(ix, indices, itype, table_stride, index_base, batch, lookups))
             return ctx_fail(ctx, DLRM_E_STATE, "dlrm_sgd_update: indexer was not built from these indices");
-        if (ix->split)
-            return ctx_fail(ctx, DLRM_E_STATE,
-                            "dlrm_sgd_update: indexer was built by dlrm_step_fwd (once-hit rows are updated by "
-                            "dlrm_step_bwd); rebuild it or call dlrm_step_bwd");
     } else {
         rc = dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, lookups);
         if (rc) return rc;
     }
     rc = ensure_partials(ctx, ix, tb->D);
     if (rc) return rc;
+    // a split indexer (dlrm_indexer_build's default form, or dlrm_step_fwd's): its once-hit
+    // positions are this launch's too
+    const SinglesArgs sa{ix->split ? ix->dev.single : nullptr, indices, itype, table_stride, index_base,
+                         batch * lookups};
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
-                            (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr);
+                            (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr, sa);
 }
 
 // ----------------------------------------------------------------------- training step
@@ -797,9 +821,12 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* 
     CHECK_ARG(flags != (DLRM_STEP_BWD_ONLY | DLRM_STEP_APPLY_ONLY), "dlrm_step_bwd: flags %u", flags);
     rc = ensure_partials(ctx, ix, tb->D);
     if (rc) return rc;
+    // the split backward (once-hit rows updated there) where the shape has it; otherwise the
+    // gather backward writes every dt row and the apply takes a split indexer's once-hit rows too
+    const bool split_bwd = ix->split && step_split_supported(tb->aligned16, tb->T, tb->dtype, d, x, x_ld);
     if (flags & DLRM_STEP_APPLY_ONLY) {
         rc = DLRM_OK;
-    } else if (ix->split) {
+    } else if (split_bwd) {
         CHECK_ARG((uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && dx_ld % 4 == 0 && dt_ld % 4 == 0,
                   "dlrm_step_bwd: dx and dt must be 16-B aligned with leading dimensions divisible by 4");
         rc = launch_step_bwd(ctx, tb->d_desc, tb->T, tb->dtype, indices, itype, table_stride, index_base, d, batch, x,
@@ -809,8 +836,12 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* 
                                         index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, nullptr);
     }
     if (rc || (flags & DLRM_STEP_BWD_ONLY)) return rc;
+    // once-hit rows: updated by the split backward, else by this apply (an unsplit indexer lists
+    // them as chunks)
+    const SinglesArgs sa{(ix->split && !split_bwd) ? ix->dev.single : nullptr, indices, itype, table_stride,
+                         index_base, batch};
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, 1, (int64_t)batch, dt,
-                            DLRM_F32, dt_ld, d, lr);
+                            DLRM_F32, dt_ld, d, lr, sa);
 }
 
 }  // extern "C"

@@ -36,6 +36,8 @@ struct ApplyGeom {
     static constexpr int RPW = 64 / LPR;
     static constexpr int NG = kApplyWaves * RPW;        // lane groups per workgroup
     static constexpr int IF = VPL >= 4 ? 4 : 16 / VPL;  // grad rows in flight per lane
+    // once-hit positions per lane group (a grad and a table row in flight for each)
+    static constexpr int SPPG = VPL * NE >= 16 ? 2 : (VPL * NE >= 8 ? 4 : 8);
 };
 
 // Cross-workgroup hand-off of slice partials (cdna_hip_programming.md Guideline 16, R1/R2):
@@ -127,6 +129,60 @@ __device__ __forceinline__ void run_chunk(const int32_t* __restrict__ perm, cons
         for (int e = 0; e < NE; ++e) tv[j][e] = __builtin_fmaf(-lr, acc[j][e], tv[j][e]);
         store_row<TT, NE>(row, (v + j * 64) * NE, tv[j]);
     }
+}
+
+// ---- once-hit positions of a split indexer (single[p] = 1: the position's row is hit by no other
+// position), SPPG consecutive positions per lane group: w = fmaf(-lr, 0 + g, w), the chunk
+// path's arithmetic for a one-position segment, with no descriptor or perm read.
+struct SinglesArgs {
+    const uint8_t* single;  // [T][cap] (IndexerDev::single); NULL: no singles items
+    const void* idx;
+    int itype;
+    int64_t tstride;
+    int base;
+    int N;                  // positions per table
+};
+template <typename TT, typename GT, int VPR>
+__device__ __forceinline__ void run_singles(const SinglesArgs& sa, int64_t cap, TT* __restrict__ table, int64_t nrows,
+                                            int t, int p0, const GT* __restrict__ gbase, int64_t grad_ld, int L,
+                                            float lr, int v, int gl0) {
+    typedef ApplyGeom<GT, VPR> G;
+    constexpr int NE = G::NE, D = G::D, LPR = G::LPR, PPG = G::SPPG;
+    constexpr int KX = (PPG + LPR - 1) / LPR;
+    uint32_t pr[KX];  // the row of position p0 + k*LPR + v, ~0u when it is not a single
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+        const int u = k * LPR + v;
+        const bool ok = u < PPG && p0 + u < sa.N;
+        const uint8_t fl = ok ? ldg<uint8_t>(sa.single + (int64_t)t * cap + p0 + u) : (uint8_t)0;
+        const int64_t r = load_index_if(ok, sa.idx, sa.itype, (int64_t)t * sa.tstride + p0 + u) - sa.base;
+        pr[k] = (fl && r >= 0 && r < nrows) ? (uint32_t)r : ~0u;
+    }
+    uint32_t ru[PPG];
+    typename Vec<GT>::type gv[PPG][G::VPL];
+    float tv[PPG][G::VPL][NE];
+#pragma unroll
+    for (int u = 0; u < PPG; ++u) {
+        ru[u] = (uint32_t)__shfl((int)pr[u / LPR], gl0 + u % LPR, 64);
+        if (ru[u] != ~0u) {
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j) {
+                gv[u][j] = grad_vec<GT>(gbase, grad_ld, L, p0 + u, v + j * 64);
+                load_row<TT, NE>(table + (int64_t)ru[u] * D, (v + j * 64) * NE, tv[u][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PPG; ++u)
+        if (ru[u] != ~0u)
+#pragma unroll
+            for (int j = 0; j < G::VPL; ++j) {
+                float g[NE];
+                Vec<GT>::to_f32(gv[u][j], g);
+#pragma unroll
+                for (int e = 0; e < NE; ++e) tv[u][j][e] = __builtin_fmaf(-lr, 0.0f + g[e], tv[u][j][e]);
+                store_row<TT, NE>(table + (int64_t)ru[u] * D, (v + j * 64) * NE, tv[u][j]);
+            }
 }
 
 // LDS of a hot-slice item (one workgroup)

@@ -218,6 +218,10 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
                                int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix);
+int launch_interact_bwd_blocked(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
+                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
+                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld);
 int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype, const void* idx,
                     int itype, int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, void* out,
                     int64_t out_ld, int padding, const IndexerDev& ix);
@@ -247,9 +251,10 @@ int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const voi
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
                          int itype, int64_t tstride, int base, int B, int L, bool split = false,
                          hipStream_t stream = nullptr);
+struct SinglesArgs;
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
-                     float lr);
+                     float lr, const SinglesArgs& singles);
 int launch_triangular_slice(dlrm_ctx* ctx, int dtype, int sz, int B, const void* z, int64_t z_bs, void* out,
                             int64_t out_ld);
 int launch_triangular_slice_back(dlrm_ctx* ctx, int dtype, int sz, int B, const void* dy, int64_t dy_ld, void* a,

@@ -117,6 +117,10 @@ struct GatherArgs {
     int base;
     int L;
     unsigned* err;
+    // backward: when set, table t's dt row of sample b goes to dt + dtb[t] + b * dtl[t] (device
+    // arrays; the sharded exchange's per-owner send layout) and dt's x row is not written
+    const int64_t* dtb;
+    const int64_t* dtl;
 };
 
 // Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
@@ -354,10 +358,18 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
     // the table descriptors, once per workgroup, in LDS after the waves' regions: read where
     // used instead of held in registers across the index loads
     TableDesc* tds = (TableDesc*)(smem + G::WPB * G::template lds_floats<UPD>());
+    int64_t* dmap = (int64_t*)(tds + (F - 1));  // GATHER + ga.dtb: [2][F-1] row bases / strides of dt
     if (GATHER) {
-        for (int t = threadIdx.x; t < F - 1; t += blockDim.x) tds[t] = load_table(ga.tabs, t);
+        for (int t = threadIdx.x; t < F - 1; t += blockDim.x) {
+            tds[t] = load_table(ga.tabs, t);
+            if (ga.dtb) {
+                dmap[t] = ga.dtb[t];
+                dmap[F - 1 + t] = ga.dtl[t];
+            }
+        }
         __syncthreads();
     }
+    const bool mapped = GATHER && ga.dtb;
     if (w >= G::WPB) return;
     const int c = lane & 15, q = lane >> 4;
     float* S = smem + w * G::template lds_floats<UPD>();
@@ -524,8 +536,10 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
 #pragma unroll
                                     for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
                                     store_row<T, 4>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
-                                } else {
+                                } else if (!mapped) {
                                     stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+                                } else if (f > 0) {
+                                    stg<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0, v);
                                 }
                                 if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo[h] + v);
                             }
@@ -926,7 +940,7 @@ static void launch_bwd_nb(hipStream_t s, int cus, int d, int F, int B, const voi
                           const GatherArgs& ga, const void* x, int64_t x_ld) {
     typedef BwdGeom<NB> G;
     const unsigned g = grid_for(B, G::WPB, cus);
-    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB + (GATHER ? sizeof(TableDesc) * (F - 1) : 0);
+    const size_t lds = sizeof(float) * G::LDS_FLOATS * G::WPB + (GATHER ? (sizeof(TableDesc) + 16) * (F - 1) : 0);
     hipLaunchKernelGGL((interact_bwd_kernel<T, NB, GATHER>), dim3(g), dim3(64 * G::WPB), lds, s, d, F, B,
                        (const T*)dout, dout_ld, (const T*)t, t_ld, dx, dx_ld, dt, dt_ld, ga, (const T*)x, x_ld);
 }
@@ -1023,6 +1037,31 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
     }
     return run_interact_bwd<true>(ctx, dtype, d, T_ + 1, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dt, dt_ld, ga,
                                   tabs_aligned16, x, x_ld);
+}
+
+// dlrm_interact_bwd_gather with table t's dt rows written to dst + dbase[t] + b * dld[t] (the
+// sharded exchange's send layout) by the backward's own stores: no dt buffer, no repack launch.
+// Vector kernel shapes only (DLRM_E_UNSUPPORTED otherwise).
+int launch_interact_bwd_blocked(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
+                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
+                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
+                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld) {
+    if (B == 0 || T_ == 0) return DLRM_OK;
+    const int F = T_ + 1;
+    const int NB = (F + 15) / 16;
+    const int esz = dtype == DLRM_F32 ? 4 : 2;
+    const bool aligned = d % 4 == 0 && tabs_aligned16 && (uintptr_t)x % (4 * esz) == 0 && (x_ld % 4) == 0 &&
+                         (uintptr_t)dx % 16 == 0 && (uintptr_t)dst % 16 == 0 && (dx_ld % 4) == 0;
+    if (!aligned || NB > 7)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "interact_bwd_blocked: 16-B aligned rows and F <= 112 needed");
+    GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx), dbase, dld};
+    hipStream_t s = ctx_stream(ctx);
+    const int cus = ctx_num_cus(ctx);
+    if (dtype == DLRM_F32)
+        dispatch_bwd<float, true>(NB, s, cus, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dst, 0, ga, x, x_ld);
+    else
+        dispatch_bwd<uint16_t, true>(NB, s, cus, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dst, 0, ga, x, x_ld);
+    return ctx_hip(ctx, hipGetLastError(), "interact_bwd_blocked launch");
 }
 
 // Shapes whose backward can take a split indexer (interact_bwd_update_kernel: F <= 32, 16-B

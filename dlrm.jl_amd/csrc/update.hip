@@ -327,13 +327,15 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 // ------------------------------------------------------------------------------ apply
 // Persistent launch, flat over tables (apply.hpp).  Work items: [0, S) = the S slices of every
 // table's hot segments (one workgroup each, handed out first: the longest chains), then
-// ceil(C / NG) items of NG chunks (one per lane group).  Workgroup b takes items b, b + grid, ...:
-// every item is short, so static striding balances, and no workgroup is launched past the work.
-template <typename TT, typename GT, int VPR>
+// ceil(C / NG) items of NG chunks (one per lane group), then (singles: a split indexer whose
+// once-hit rows are this launch's too) T * ceil(N / (NG * SPPG)) items of once-hit
+// positions.  Workgroup b takes items b, b + grid, ...: every item is short, so static striding
+// balances, and no workgroup is launched past the work.
+template <typename TT, typename GT, int VPR, bool SG>
 __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_,
                                                                   int L, const GT* __restrict__ grad, int64_t grad_ld,
                                                                   int64_t grad_offset, float lr,
-                                                                  const unsigned* __restrict__ err) {
+                                                                  const unsigned* __restrict__ err, SinglesArgs sa) {
     // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
     // this step): the reference's gather throws before update!, so no table row is written
     if (*err) return;
@@ -345,9 +347,22 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     const int gid = w * G::RPW + g;
     const TableScan sS = scan_counts(ix, T_, CNT_S);
     const TableScan sC = scan_counts(ix, T_, CNT_C);
-    const int items = sS.total + (sC.total + NG - 1) / NG;
+    const int citems = sS.total + (sC.total + NG - 1) / NG;
+    constexpr int SP = NG * G::SPPG;                           // positions per singles item
+    const int per_t = SG ? (sa.N + SP - 1) / SP : 0;          // singles items per real table
+    const int items = citems + (T_ >> ix.vshift) * per_t;
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        APPLY_START(item >= sS.total ? 1 : 2);
+        APPLY_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2));
+        if (SG && item >= citems) {  // uniform: once-hit positions of one real table
+            const int t = (item - citems) / per_t;
+            const int p0 = ((item - citems) - t * per_t) * SP + gid * G::SPPG;
+            if (g >= G::RPW) continue;
+            const TableDesc td = load_table(tabs, t);
+            run_singles<TT, GT, VPR>(sa, ix.cap, (TT*)td.data, td.nrows, t, p0, grad + grad_offset + (int64_t)t * D,
+                                     grad_ld, L, lr, v, lane - v);
+            APPLY_END();
+            continue;
+        }
         if (item >= sS.total) {
             int tc, cl;
             locate(ix, T_, CNT_C, sC, (item - sS.total) * NG + gid, tc, cl);
@@ -410,6 +425,26 @@ __global__ __launch_bounds__(256) void sgd_hot_scalar(IndexerDev ix, TableDesc* 
             acc += to_f32(grad[(int64_t)(ix.perm[off + i] / L) * grad_ld + grad_offset + (int64_t)(t >> ix.vshift) * D + c]);
         TT* row = table + (int64_t)(uint32_t)hd.z * D;
         row[c] = from_f32<TT>(__builtin_fmaf(-lr, acc, to_f32(row[c])));
+    }
+}
+
+template <typename TT, typename GT>
+__global__ __launch_bounds__(256) void sgd_singles_scalar(SinglesArgs sa, int64_t cap, TableDesc* __restrict__ tabs,
+                                                          int D, int L, const GT* __restrict__ grad, int64_t grad_ld,
+                                                          int64_t grad_offset, float lr,
+                                                          const unsigned* __restrict__ err) {
+    if (*err) return;
+    const int t = blockIdx.y;
+    const int64_t total = (int64_t)sa.N * D;
+    TT* table = (TT*)tabs[t].data;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(e / D), c = (int)(e % D);
+        if (!sa.single[(int64_t)t * cap + p]) continue;
+        const int64_t r = load_index(sa.idx, sa.itype, (int64_t)t * sa.tstride + p) - sa.base;
+        if (r < 0 || r >= tabs[t].nrows) continue;
+        const float g = to_f32(grad[(int64_t)(p / L) * grad_ld + grad_offset + (int64_t)t * D + c]);
+        TT* row = table + r * D;
+        row[c] = from_f32<TT>(__builtin_fmaf(-lr, 0.0f + g, to_f32(row[c])));
     }
 }
 
@@ -495,15 +530,18 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
 
 template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
-                             int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err) {
+                             int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err,
+                             const SinglesArgs& sa) {
     typedef ApplyGeom<GT, VPR> G;
     // persistent grid: resident workgroups only (never more than the worst-case item count per
-    // table: N / kHotSlice + N / (kChunk + 1) + 1 hot slices, N / NG chunk items)
-    const int64_t ib = (int64_t)T_ * (N / kHotSlice + N / (kChunk + 1) + 1 + (N + G::NG - 1) / G::NG);
+    // table: N / kHotSlice + N / (kChunk + 1) + 1 hot slices, N / NG chunk items, singles items)
+    const int64_t SP = G::NG * G::SPPG;
+    const int64_t ib = (int64_t)T_ * (N / kHotSlice + N / (kChunk + 1) + 1 + (N + G::NG - 1) / G::NG) +
+                       (sa.single ? (int64_t)(T_ >> ix.vshift) * ((N + SP - 1) / SP) : 0);
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR>, kApplyThreads, 0) !=
-                hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR, false>, kApplyThreads,
+                                                         0) != hipSuccess || per_cu < 1)
             per_cu = 1;
     }
     int dev = 0, cus = 0;
@@ -511,16 +549,23 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t grid = (int64_t)per_cu * (cus > 0 ? cus : 256);
     if (grid > ib) grid = ib;
-    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kApplyThreads), 0,
-                       s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err);
+    // (the once-hit items are a separate instantiation: the step's apply stays lean)
+    if (sa.single)
+        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, true>), dim3((unsigned)(grid < 1 ? 1 : grid)),
+                           dim3(kApplyThreads), 0, s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
+                           sa);
+    else
+        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, false>), dim3((unsigned)(grid < 1 ? 1 : grid)),
+                           dim3(kApplyThreads), 0, s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
+                           sa);
 }
 
 template <typename TT, typename GT>
 static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L,
                            const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, int64_t N,
-                           const unsigned* err) {
+                           const unsigned* err, const SinglesArgs& sa) {
 #define DLRM_CASE(V) \
-    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err); return true;
+    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa); return true;
     switch (vpr) {
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64) DLRM_CASE(128)
         default: return false;
@@ -530,7 +575,7 @@ static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDe
 
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T_, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
-                     float lr) {
+                     float lr, const SinglesArgs& sa) {
     if (T_ == 0 || N == 0) return DLRM_OK;
     T_ <<= ix.vshift;  // virtual tables (row-parity halves) of a forward-launch build
     hipStream_t s = ctx_stream(ctx);
@@ -544,13 +589,14 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     if (aligned && slots < (1ll << 31)) {
         const int vpr = D * gesz / 16;
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
-            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
+            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
         else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32)
-            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
+            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
         else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16)
-            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
+            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
         else
-            done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err);
+            done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N,
+                                                      err, sa);
     }
     if (!done) {
         const int64_t gx0 = (N * D + 255) / 256;
@@ -561,7 +607,10 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     hipLaunchKernelGGL((sgd_chunks_scalar<TT, GT>), dim3(gx, T_), dim3(256), 0, s, ix, tabs, D, L, (const GT*)grad, \
                        grad_ld, grad_offset, lr, err);                                                              \
     hipLaunchKernelGGL((sgd_hot_scalar<TT, GT>), dim3(hx, T_), dim3(256), 0, s, ix, tabs, D, L, (const GT*)grad,    \
-                       grad_ld, grad_offset, lr, err);
+                       grad_ld, grad_offset, lr, err);                                                              \
+    if (sa.single)                                                                                                  \
+        hipLaunchKernelGGL((sgd_singles_scalar<TT, GT>), dim3(gx, T_ >> ix.vshift), dim3(256), 0, s, sa, ix.cap,    \
+                           tabs, D, L, (const GT*)grad, grad_ld, grad_offset, lr, err);
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32) { DLRM_SCALAR(float, float) }
         else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32) { DLRM_SCALAR(uint16_t, float) }
         else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16) { DLRM_SCALAR(float, uint16_t) }

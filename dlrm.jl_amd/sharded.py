@@ -13,9 +13,9 @@ way moves the looked-up vectors to the ranks that own the samples, and their gra
             every table's B vectors for r's samples are now one contiguous [B][D] block of
             recv, i.e. a B-row table whose row b is sample b: the fused lookup+interaction
             kernel runs on these T "received tables" with identity indices (no ys copy)
-  backward: dot_back re-gathers T from the received tables (dlrm_interact_bwd_gather)
-            -> dt [B][F*D]; dt's table columns scattered per owner (dlrm_scatter_rows)
-                                                            -> gsend [dst j][B][T_j][D]
+  backward: dot_back re-gathers T from the received tables and stores each table's gradient
+            rows straight into the send layout (dlrm_interact_bwd_blocked; other ops: dt
+            [B][F*D], then dlrm_scatter_rows)                -> gsend [dst j][B][T_j][D]
             all-to-all                                      -> grecv [src i][B][T_r][D]
                                                                = grad [Bg][T_r*D]
             update!(Descent) of r's tables with r's indices for all Bg samples; the
@@ -148,6 +148,19 @@ class HipShardOps:
                                                    dout.stride(0), padding, ptr(dx), dx.stride(0), ptr(dt),
                                                    dt.stride(0)))
 
+    def interact_bwd_send(self, dout, x, dx, gsend, dbase, dld, padding):
+        """dot_back on the received tables with every table's dt rows stored straight into the
+        exchange's send layout (one launch: dlrm_interact_bwd_blocked).  False: shape not
+        supported by the fused kernel (the caller repacks dt instead)."""
+        i = self.ident
+        rc = self.lib.dlrm_interact_bwd_blocked(self.ctx.bind(), self.rts.handle, ptr(i.data), i.itype, i.stride, 0,
+                                                i.B, ptr(x), x.stride(0), ptr(dout), dout.stride(0), padding, ptr(dx),
+                                                dx.stride(0), ptr(gsend), ptr(dbase), ptr(dld))
+        if rc == _lib.E_UNSUPPORTED:
+            return False
+        self._ok(rc)
+        return True
+
     def update(self, idx, grad, prebuilt=False):
         flags = _lib.UPDATE_PREBUILT if prebuilt else 0
         self._ok(self.lib.dlrm_sgd_update(self.ctx.bind(), self.ts.handle, self.indexer.handle, flags, ptr(idx.data),
@@ -178,7 +191,7 @@ class ShardedHotPath:
         self.recv = torch.empty((T * B * D,), dtype=dtype, device=dev)
         self.out = torch.empty((B, self.width), dtype=dtype, device=dev)
         self.dx = torch.empty((B, D), dtype=torch.float32, device=dev)
-        self.dt = torch.empty((B, self.F * D), dtype=torch.float32, device=dev)
+        self.dt = None  # [B][F*D] fp32, only where the backward cannot store into gsend directly
         self.gsend = torch.empty((T * B * D,), dtype=torch.float32, device=dev)
         self.grecv = torch.empty((W * Tr * B * D,), dtype=torch.float32, device=dev)
         self.grad = self.grecv.view(self.Bg, Tr * D) if Tr else None
@@ -210,6 +223,7 @@ class ShardedHotPath:
         elif exchange != "torch":
             raise ValueError(f"exchange must be 'torch' or 'abi', not {exchange!r}")
         self._graphs = None
+        self._fused_bwd = None  # None: not tried yet; False: the ops cannot (repack instead)
         self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
 
     # ---- exchange (pure data movement; identical for every ShardOps)
@@ -255,6 +269,18 @@ class ShardedHotPath:
 
     def seg_interact(self, x, dout):
         self.ops.interact_fwd_recv(x, self.out, self.padding)
+        self.interact_bwd(dout, x)
+
+    def interact_bwd(self, dout, x):
+        """dot_back, its table gradients in the exchange layout: one launch where the ops offer it
+        (the backward's stores go straight to gsend), else dt + the repack."""
+        send = getattr(self.ops, "interact_bwd_send", None)
+        if send is not None and self._fused_bwd is not False:
+            self._fused_bwd = send(dout, x, self.dx, self.gsend, self.gs_base, self.gs_ld, self.padding)
+            if self._fused_bwd:
+                return
+        if self.dt is None:
+            self.dt = torch.empty((self.B, self.F * self.D), dtype=torch.float32, device=self.dx.device)
         self.ops.interact_bwd_recv(dout, x, self.dx, self.dt, self.padding)
         self.pack_grad()
 
@@ -270,8 +296,7 @@ class ShardedHotPath:
         return self.out
 
     def backward(self, idx, dout, x):
-        self.ops.interact_bwd_recv(dout, x, self.dx, self.dt, self.padding)
-        self.pack_grad()
+        self.interact_bwd(dout, x)
         self.exchange_bwd()
         self.seg_update(idx)
         return self.dx

@@ -234,6 +234,17 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tables, dlrm_inde
                              const void* dout, int64_t dout_ld, int padding,
                              float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 
+/* dlrm_interact_bwd_gather for the table-sharded backward: dx as there, and table t's dt row of
+ * sample b written straight to dst + dst_base[t] + b * dst_ld[t] (fp32; dst_base / dst_ld device
+ * arrays of num_tables int64 elements, the send layout of dlrm_alltoall_bwd), i.e. the backward
+ * and dlrm_scatter_rows in one launch; dt's x rows are not written.  Needs 16-B aligned rows, x,
+ * dx and dst (DLRM_E_UNSUPPORTED otherwise).  No reference counterpart. */
+int dlrm_interact_bwd_blocked(dlrm_ctx* ctx, const dlrm_tables* tables,
+                              const void* indices, int itype, int64_t table_stride, int index_base,
+                              int batch, const void* x, int64_t x_ld, const void* dout, int64_t dout_ld,
+                              int padding, float* dx, int64_t dx_ld, float* dst,
+                              const int64_t* dst_base, const int64_t* dst_ld);
+
 /* update!(Descent(lr), tables, grads, indexers):
  *   table_t[r] -= lr * sum_{(b,k): idx_t[b*lookups+k] - base == r} grad[b][grad_offset + t*dim + :]
  * Default: deterministic (sum in ascending position order per unique row, one

@@ -540,9 +540,9 @@ def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
 
 
 def test_step_api_state_and_bounds(pkg, gpu):
-    """A split indexer is refused by the plain update; step_bwd needs step_fwd's indices; an
-    out-of-range index raises BoundsError and the step still matches the operator sequence on
-    the valid positions."""
+    """The forward's split indexer also drives the plain update (once-hit rows included, bit for
+    bit the update of a fresh build); step_bwd needs step_fwd's indices; an out-of-range index
+    raises BoundsError and the step still matches the operator sequence on the valid positions."""
     rows, D, B = [100, 7, 5000], 16, 256
     rng = np.random.default_rng(3)
     tabs = rand_tables(rng, rows, D)
@@ -553,9 +553,13 @@ def test_step_api_state_and_bounds(pkg, gpu):
     dout = torch.randn((B, hp.width), device=gpu)
     p = pkg.PackedIndices(idx)
     hp.step_fwd(x, p)
-    with pytest.raises(pkg.DLRMError) as e:
-        hp.sgd_update(p, prebuilt=True)
-    assert e.value.code == pkg._lib.E_STATE
+    g = torch.randn((B, hp.F * D), device=gpu)
+    hp.dt.copy_(g)
+    hp.sgd_update(p, prebuilt=True)
+    ts_ref = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    pkg.update_(pkg.Descent(1.0), ts_ref, pkg.maplookup_pullback(D, ts_ref, p, g), index_base=0)
+    for a, b in zip(hp.ts, ts_ref):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
     other = pkg.PackedIndices(idx.clone())
     with pytest.raises(pkg.DLRMError) as e:
         hp.step_bwd(dout, x=x, idx=other)
