@@ -53,9 +53,12 @@ def parse():
     ap.add_argument("--nbatch", type=int, default=NBATCH, help="distinct index batches cycled")
     ap.add_argument("--sustain", type=float, default=2.0,
                     help="seconds of back-to-back steps timed after the K-step region (reported as 'sustained')")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: build the next batch's indexer on a side stream during each step (step API only; "
-                         "measured slower: 57.5 vs 49.6 us, the graph runs the side branch serially)")
+    ap.add_argument("--pipeline", type=int, default=-1,
+                    help="where the step's indexer is built: 0 in the forward's launch; 2 inside the previous "
+                         "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 on a side "
+                         "stream (measured slower: a replayed graph runs the side branch serially); -1 (default): 2 "
+                         "for dim <= 32 (the forward is the indexer's length: D=16 measured 10.9 + 12.7 us vs "
+                         "14.6 + 9.2), else 0 (the gather is the forward's length: D=128 14.0 + 12.9 vs 15.2 + 10.7)")
     return ap.parse_args()
 
 
@@ -218,6 +221,8 @@ def main():
             dist.init_process_group(backend)
     w = dict(pkg.WORKLOADS[a.workload])
     B, D, L = w["batch"], w["dim"], w["lookups"]
+    if a.pipeline < 0:
+        a.pipeline = 2 if D <= 32 else 0
     if a.mode == "auto":
         a.mode = "eager" if (L > 1 and world == 1) else "graph"
     rows = w["rows"]
@@ -232,7 +237,7 @@ def main():
                              overlap_indexer=None if a.overlap_indexer < 0 else bool(a.overlap_indexer),
                              fused=bool(a.fused),
                              materialize_ys=None if a.materialize_ys < 0 else bool(a.materialize_ys),
-                             pipeline=bool(a.pipeline))
+                             pipeline={0: None, 1: "side", 2: "apply"}[a.pipeline])
         F = T + 1
         dtp = tables[0].dtype
         x = torch.randn((B, D), device=dev, generator=g).to(dtp)
@@ -241,7 +246,10 @@ def main():
         for p in packs:
             engine.validate(x, p, dout)
 
-        if engine.pipeline:
+        if engine.pipeline == "apply":
+            def step(k):
+                engine.step_prep(x, packs[k % nb], dout, packs[(k + 1) % nb])
+        elif engine.pipeline:
             def step(k):
                 engine.step_next(x, packs[k % nb], dout, packs[(k + 1) % nb])
         else:
@@ -280,8 +288,13 @@ def main():
     nb = a.nbatch
     chunk = min(CHUNK, nb)
     graphs = {}
-    if world == 1 and engine.pipeline:
-        engine.prime(packs[0])  # the captured steps start at batch 0
+    def prime():
+        """Pipelined steps: the indexer the first step of a run reads holds batch 0 (a run starts
+        at batch 0; the graphs were captured from this state)."""
+        if world == 1 and engine.pipeline:
+            engine.prime(packs[0], x=x, dout=dout, prev=packs[nb - 1])
+
+    prime()
 
     def capture(start, n):
         cur = torch.cuda.current_stream()
@@ -328,6 +341,7 @@ def main():
             graphs[piece].replay()
 
     def timed(n):
+        prime()  # (outside the timed region)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -389,7 +403,7 @@ def main():
         if engine.step_api:
             sts = [index_stats(packs[k].data.reshape(T, B * L).cpu().numpy()) for k in range(nb)]
             st = {key: sum(v[key] for v in sts) / nb for key in sts[0]}
-            bytes_ = step_api_bytes(B, T, D, L, E, 4, st, pipelined=engine.pipeline)
+            bytes_ = step_api_bytes(B, T, D, L, E, 4, st, pipelined=bool(engine.pipeline))
             for k in range(nb):  # batch k's split indexer, built by its own step forward
                 engine.indexer = indexers[k]
                 engine.step_fwd(x, packs[k])
@@ -405,7 +419,20 @@ def main():
             engine.interact_bwd(dout, x=x, idx=packs[k], build_indexer=True)
             engine.indexer = home
 
-        if engine.pipeline:  # indexer on the side stream, built for the next batch
+        if engine.pipeline == "apply":  # the next batch's indexer built by the apply launch
+            names = ["lookup_interact_fwd", "interact_bwd", "sgd_update"]
+            nxt = [pkg.SparseIndexer(T, B * L, dev) for _ in range(2)]
+
+            def apply_prep_k(k):
+                engine.indexer = indexers[k]
+                engine.step_bwd(dout, x=x, idx=packs[k], flags=pkg._lib.STEP_APPLY_ONLY,
+                                prepare=(nxt[k % 2], packs[(k + 1) % nb]))
+                engine.indexer = home
+
+            fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: sbwd_k(k, pkg._lib.STEP_BWD_ONLY),
+                   apply_prep_k]
+            bytes_["sgd_update"] += bytes_["indexer_build"]
+        elif engine.pipeline:  # indexer on the side stream, built for the next batch
             names = ["lookup_interact_fwd", "interact_bwd", "sgd_update", "indexer_build"]
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: sbwd_k(k, pkg._lib.STEP_BWD_ONLY),
                    lambda k: sbwd_k(k, pkg._lib.STEP_APPLY_ONLY),
@@ -464,7 +491,8 @@ def main():
             stages[n] = {"us": round(us, 2), "alg_bytes": int(bytes_[n]),
                          "GBps": round(bytes_[n] / (us * 1e-6) / 1e9, 1)}
         # the dominant kernel of the step's critical path (a side-stream stage overlaps it)
-        dom = max((n for n in names if not (engine.pipeline and n == "indexer_build")), key=lambda n: stages[n]["us"])
+        dom = max((n for n in names if not (engine.pipeline == "side" and n == "indexer_build")),
+                  key=lambda n: stages[n]["us"])
         ach = stages[dom]["GBps"]
         roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(a.workload, dom),
@@ -501,7 +529,11 @@ def main():
                                   else "eager"),
                        "ys": ("received blocks read in place (no ys)" if world > 1 else "materialized"
                               if engine.materialize_ys else "not materialized (backward re-gathers T)"),
-                       "step": ("fused forward + dlrm_step_bwd (once-hit rows updated in the backward); the next "
+                       "step": ("3 launches: fused lookup + interaction (gather only) / dlrm_step_bwd_prepare = "
+                                "interaction backward with once-hit rows updated + apply of repeated rows, whose launch "
+                                "also builds the next batch's indexer"
+                                if world == 1 and engine.pipeline == "apply" else
+                                "fused forward + dlrm_step_bwd (once-hit rows updated in the backward); the next "
                                 "batch's indexer built on a side stream during the step"
                                 if world == 1 and engine.pipeline else
                                 "dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "

@@ -108,6 +108,8 @@ SIGNATURES = {
     "dlrm_step_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32]),
     "dlrm_step_bwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
                              _i64, _f32, _u32]),
+    "dlrm_step_bwd_prepare": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64,
+                                     _vp, _i64, _f32, _vp, _vp, _u32]),
 }
 
 _lib = None

@@ -47,6 +47,8 @@ struct dlrm_indexer {
     // recorded by the last build
     bool built = false;
     bool split = false;  // built by dlrm_step_fwd's kernel: once-hit rows are left to the backward
+    bool prepared = false;  // built by dlrm_step_bwd_prepare for the next dlrm_step_fwd (not yet consumed)
+    unsigned* prep_err = nullptr;  // device word: bounds errors of a prepared build (the forward re-raises)
     const void* indices = nullptr;
     int itype = 0, base = 0, B = 0, L = 0;
     int64_t tstride = 0;
@@ -78,10 +80,22 @@ int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what) {
 
 static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice"); }
 
+// parts per table in the step forward's indexer (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides, for
+// comparison)
+static int step_parts_log2() {
+    static const int parts_log2 = [] {
+        const char* e = getenv("DLRM_STEP_PARTS");
+        const int p = e ? atoi(e) : kStepParts;
+        return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
+    }();
+    return parts_log2;
+}
+
 static void record_build(dlrm_indexer* ix, bool split, const void* indices, int itype, int64_t tstride, int base,
                          int B, int L) {
     ix->built = true;
     ix->split = split;
+    ix->prepared = false;
     ix->indices = indices;
     ix->itype = itype;
     ix->tstride = tstride;
@@ -535,6 +549,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.hot_slice, n * 16}, {(void**)&ix->dev.hot_cnt, n * 4},
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
+        {(void**)&ix->prep_err, 16},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
         {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
         {(void**)&ix->dev.hseg, (size_t)(T0 * hs) * 8},
@@ -738,15 +753,16 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     const int64_t P = (int64_t)F * (F - 1) / 2;
     CHECK_ARG(padding >= 0 && x_ld >= d && out_ld >= d + P + padding, "dlrm_step_fwd: leading dimensions too small");
     CHECK_ARG(batch == 0 || (x && out), "dlrm_step_fwd: null buffer");
+    if (ix->prepared && built_from(ix, indices, itype, table_stride, index_base, batch, 1)) {
+        // built by the previous step's apply launch (dlrm_step_bwd_prepare): the gather alone
+        ix->prepared = false;
+        rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
+                                        index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding);
+        if (rc != DLRM_E_UNSUPPORTED) return rc;  // (no fused forward for this x: build below)
+    }
+    ix->prepared = false;
     ix->built = false;
-    // parts per table in the forward launch's indexer (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides, for
-    // comparison)
-    static const int parts_log2 = [] {
-        const char* e = getenv("DLRM_STEP_PARTS");
-        const int p = e ? atoi(e) : kStepParts;
-        return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
-    }();
-    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? parts_log2 : 0;
+    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? step_parts_log2() : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev);
     if (rc == DLRM_OK) {
@@ -804,10 +820,10 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     return dlrm_indexer_build(ctx, ix, tb, indices, itype, table_stride, index_base, batch, 1);
 }
 
-int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
-                  int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld, const void* dout,
-                  int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr,
-                  unsigned flags) {
+static int step_bwd_impl(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
+                         int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld,
+                         const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dt,
+                         int64_t dt_ld, float lr, unsigned flags, const PrepArgs* prep) {
     CHECK_ARG(ctx && tb && ix, "dlrm_step_bwd: null ctx/tables/indexer");
     int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
     if (rc) return rc;
@@ -841,7 +857,47 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* 
     const SinglesArgs sa{(ix->split && !split_bwd) ? ix->dev.single : nullptr, indices, itype, table_stride,
                          index_base, batch};
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, 1, (int64_t)batch, dt,
-                            DLRM_F32, dt_ld, d, lr, sa);
+                            DLRM_F32, dt_ld, d, lr, sa, prep);
+}
+
+int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
+                  int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld, const void* dout,
+                  int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr,
+                  unsigned flags) {
+    return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,
+                         dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
+}
+
+int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const void* indices, int itype,
+                          int64_t table_stride, int index_base, int batch, const void* x, int64_t x_ld,
+                          const void* dout, int64_t dout_ld, int padding, float* dx, int64_t dx_ld, float* dt,
+                          int64_t dt_ld, float lr, dlrm_indexer* next, const void* next_indices, unsigned flags) {
+    CHECK_ARG(ctx && tb && ix && next && next != ix, "dlrm_step_bwd_prepare: null or shared indexer");
+    CHECK_ARG(next->T == tb->T && batch <= next->dev.cap, "dlrm_step_bwd_prepare: next indexer too small");
+    int rc = check_indices(ctx, tb, next_indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    // the next batch's build runs as extra workgroups of this step's apply launch: the step
+    // forward's split build (the same parts), so the next dlrm_step_fwd only gathers
+    const int NB = (tb->T + 1 + 15) / 16;
+    const bool inapply = batch > 0 && tb->T > 0 && batch <= kStepIndexMaxN && NB <= 2 && tb->aligned16 &&
+                         next->TV == kStepMaxParts * next->T;
+    if (!inapply)  // no pipelined form for this shape: the plain step (the next forward builds)
+        return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
+                             padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
+    if (flags & DLRM_STEP_BWD_ONLY)  // (the next build rides on the apply launch)
+        return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
+                             padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
+    next->built = false;
+    next->prepared = false;
+    next->dev.vshift = step_parts_log2();
+    const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
+                      next->prep_err};
+    rc = step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,
+                       dx, dx_ld, dt, dt_ld, lr, flags, &pa);
+    if (rc) return rc;
+    record_build(next, true, next_indices, itype, table_stride, index_base, batch, 1);
+    next->prepared = true;
+    return DLRM_OK;
 }
 
 }  // extern "C"

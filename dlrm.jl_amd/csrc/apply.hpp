@@ -185,6 +185,21 @@ __device__ __forceinline__ void run_singles(const SinglesArgs& sa, int64_t cap, 
             }
 }
 
+// The NEXT batch's split indexer, built by extra workgroups of this apply launch (the training
+// step's pipelined form: dlrm_step_bwd_prepare).  Its bounds errors go to `err` (private: the next
+// step's forward gathers the same indices and raises them on the context's flag).
+struct PrepArgs {
+    IndexerDev ix;
+    const TableDesc* tabs;  // the tables (for nrows)
+    int T;                  // real tables
+    const void* idx;
+    int itype;
+    int64_t tstride;
+    int base;
+    int N;
+    unsigned* err;
+};
+
 // LDS of a hot-slice item (one workgroup)
 template <int D>
 struct SliceLds {

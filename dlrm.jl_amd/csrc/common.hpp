@@ -252,9 +252,10 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
                          int itype, int64_t tstride, int base, int B, int L, bool split = false,
                          hipStream_t stream = nullptr);
 struct SinglesArgs;
+struct PrepArgs;
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
-                     float lr, const SinglesArgs& singles);
+                     float lr, const SinglesArgs& singles, const PrepArgs* prep = nullptr);
 int launch_triangular_slice(dlrm_ctx* ctx, int dtype, int sz, int B, const void* z, int64_t z_bs, void* out,
                             int64_t out_ld);
 int launch_triangular_slice_back(dlrm_ctx* ctx, int dtype, int sz, int B, const void* dy, int64_t dy_ld, void* a,

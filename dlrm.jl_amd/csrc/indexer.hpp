@@ -459,6 +459,16 @@ __device__ void fast_index_table(const IndexerDev& ix, int v, int t, int vs, uin
     PHASE(22);
 }
 
+// The training step's split build, as extra 256-thread workgroups of another launch (the step
+// forward's, interact.hip; or the previous step's apply, update.hip): one per virtual table.
+constexpr int kStepIndexEPL = kStepIndexMaxN / 256;  // positions per thread
+#ifndef DLRM_STEP_DB
+#define DLRM_STEP_DB 8
+#endif
+// 8-bit digits: a table part holds about N >> vshift positions, and the digit scan (NW << DB
+// counters) is a fixed cost of every counting pass
+typedef FastLds<256, kStepIndexEPL, DLRM_STEP_DB> StepLds;
+
 // ------------------------------------------------- flat (table, item) lookup over counts
 // Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
 // may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.

@@ -35,6 +35,11 @@ __device__ unsigned long long g_phase_fwd[64];
 extern "C" int dlrm_debug_phase_fwd(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_fwd), sizeof(g_phase_fwd));
 }
+extern "C" int dlrm_debug_phase_fwd_reset(void) {
+    static unsigned long long z[64];
+    for (int k = 0; k < 64; ++k) z[k] = (k == 60 || k == 62) ? ~0ull : 0ull;
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_fwd), z, sizeof(z));
+}
 #endif
 #include "indexer.hpp"
 
@@ -282,13 +287,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F,
 // vshift = 1 two per table, one per row parity, which halves the critical path), the rest run
 // the fused lookup + interaction without ys.  The indexer depends only on the indices, so it
 // streams beside the gather instead of adding a launch.
-constexpr int kStepIndexEPL = kStepIndexMaxN / 256;  // positions per thread
-#ifndef DLRM_STEP_DB
-#define DLRM_STEP_DB 8
-#endif
-// 8-bit digits: a table part holds about N >> vshift positions, and the digit scan (NW << DB
-// counters) is a fixed cost of every counting pass
-typedef FastLds<256, kStepIndexEPL, DLRM_STEP_DB> StepLds;
+// (StepLds, kStepIndexEPL: indexer.hpp)
 template <typename T, int NB, int DC = 0>
 __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                  int64_t x_ld, T* __restrict__ out, int64_t out_ld,
@@ -296,15 +295,32 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int T_ = F - 1;
     const int NI = T_ << ix.vshift;
+#ifdef DLRM_PHASE
+    // [0] this block's start (the traced indexer block), [60] / [61] first start / last end of any
+    // gather block, [62] / [63] first start / last end of any indexer block
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = wall_clock64();
+        if ((int)blockIdx.x == DLRM_PHASE) g_phase_fwd[0] = t0;
+        atomicMin(&g_phase_fwd[(int)blockIdx.x < NI ? 62 : 60], t0);
+    }
+#endif
     if ((int)blockIdx.x < NI) {
         StepLds& sl = *(StepLds*)smem;
         const int v = blockIdx.x, t = v >> ix.vshift;
         fast_index_table<256, kStepIndexEPL, true>(ix, v, t, ix.vshift, (uint32_t)ga.tabs[t].nrows, ga.idx, ga.itype,
                                                    ga.tstride, ga.base, B * ga.L, ga.err, sl);
+#ifdef DLRM_PHASE
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&g_phase_fwd[63], wall_clock64());
+#endif
         return;
     }
     fwd_body<T, NB, true, 4, false, DC>(blockIdx.x - NI, gridDim.x - NI, smem, d, F, B, x, x_ld, nullptr, 0, out,
                                         out_ld, padding, ga);
+#ifdef DLRM_PHASE
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&g_phase_fwd[61], wall_clock64());
+#endif
 }
 
 // ---------------------------------------------------------------------------------- bwd

@@ -331,11 +331,29 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 // once-hit rows are this launch's too) T * ceil(N / (NG * SPPG)) items of once-hit
 // positions.  Workgroup b takes items b, b + grid, ...: every item is short, so static striding
 // balances, and no workgroup is launched past the work.
-template <typename TT, typename GT, int VPR, bool SG>
+// MODE 0: chunks + hot slices; 1: + once-hit (singles) items; 2: + the next batch's split indexer
+// in the first pa.T << pa.ix.vshift workgroups (PrepArgs).
+template <typename TT, typename GT, int VPR, int MODE>
 __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_,
                                                                   int L, const GT* __restrict__ grad, int64_t grad_ld,
                                                                   int64_t grad_offset, float lr,
-                                                                  const unsigned* __restrict__ err, SinglesArgs sa) {
+                                                                  const unsigned* __restrict__ err, SinglesArgs sa,
+                                                                  PrepArgs pa) {
+    constexpr bool SG = MODE == 1;
+    int bid = blockIdx.x, nblk = gridDim.x;
+    if (MODE == 2) {
+        extern __shared__ __attribute__((aligned(16))) unsigned char prep_lds[];
+        const int NI = pa.T << pa.ix.vshift;
+        if (bid < NI) {
+            const int vv = bid, t = vv >> pa.ix.vshift;
+            fast_index_table<256, kStepIndexEPL, true>(pa.ix, vv, t, pa.ix.vshift, (uint32_t)load_table(pa.tabs, t).nrows,
+                                                       pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
+                                                       *(StepLds*)prep_lds);
+            return;
+        }
+        bid -= NI;
+        nblk -= NI;
+    }
     // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
     // this step): the reference's gather throws before update!, so no table row is written
     if (*err) return;
@@ -351,7 +369,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     constexpr int SP = NG * G::SPPG;                           // positions per singles item
     const int per_t = SG ? (sa.N + SP - 1) / SP : 0;          // singles items per real table
     const int items = citems + (T_ >> ix.vshift) * per_t;
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    for (int item = bid; item < items; item += nblk) {
         APPLY_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2));
         if (SG && item >= citems) {  // uniform: once-hit positions of one real table
             const int t = (item - citems) / per_t;
@@ -383,6 +401,14 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
                                sm);
         APPLY_END();
     }
+}
+
+// The step indexer's workgroups alone (PrepArgs), where the apply has no vector kernel to host them.
+__global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int vv = blockIdx.x, t = vv >> pa.ix.vshift;
+    fast_index_table<256, kStepIndexEPL, true>(pa.ix, vv, t, pa.ix.vshift, (uint32_t)load_table(pa.tabs, t).nrows,
+                                               pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err, *(StepLds*)lds);
 }
 
 // Generic (any D) versions: one thread per element column.
@@ -531,7 +557,7 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
 template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
                              int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err,
-                             const SinglesArgs& sa) {
+                             const SinglesArgs& sa, const PrepArgs* pa) {
     typedef ApplyGeom<GT, VPR> G;
     // persistent grid: resident workgroups only (never more than the worst-case item count per
     // table: N / kHotSlice + N / (kChunk + 1) + 1 hot slices, N / NG chunk items, singles items)
@@ -540,7 +566,7 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
                        (sa.single ? (int64_t)(T_ >> ix.vshift) * ((N + SP - 1) / SP) : 0);
     static int per_cu = 0;
     if (!per_cu) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR, false>, kApplyThreads,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sgd_apply_kernel<TT, GT, VPR, 0>, kApplyThreads,
                                                          0) != hipSuccess || per_cu < 1)
             per_cu = 1;
     }
@@ -549,23 +575,33 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t grid = (int64_t)per_cu * (cus > 0 ? cus : 256);
     if (grid > ib) grid = ib;
-    // (the once-hit items are a separate instantiation: the step's apply stays lean)
-    if (sa.single)
-        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, true>), dim3((unsigned)(grid < 1 ? 1 : grid)),
-                           dim3(kApplyThreads), 0, s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
-                           sa);
-    else
-        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, false>), dim3((unsigned)(grid < 1 ? 1 : grid)),
-                           dim3(kApplyThreads), 0, s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
-                           sa);
+    if (grid < 1) grid = 1;
+    // (the once-hit items and the next batch's indexer are separate instantiations: the step's
+    // apply stays lean)
+    if (pa) {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)sizeof(StepLds));
+        (void)attr;
+        const int NI = pa->T << pa->ix.vshift;
+        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
+                           sizeof(StepLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
+                           *pa);
+    } else if (sa.single) {
+        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 1>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
+                           tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});
+    } else {
+        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 0>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
+                           tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});
+    }
 }
 
 template <typename TT, typename GT>
 static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L,
                            const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, int64_t N,
-                           const unsigned* err, const SinglesArgs& sa) {
+                           const unsigned* err, const SinglesArgs& sa, const PrepArgs* pa) {
 #define DLRM_CASE(V) \
-    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa); return true;
+    case V: launch_apply_vec<TT, GT, V>(s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa, pa); return true;
     switch (vpr) {
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64) DLRM_CASE(128)
         default: return false;
@@ -575,7 +611,7 @@ static bool dispatch_apply(int vpr, hipStream_t s, const IndexerDev& ix, TableDe
 
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T_, int D,
                      int tdtype, int L, int64_t N, const void* grad, int gdtype, int64_t grad_ld, int64_t grad_offset,
-                     float lr, const SinglesArgs& sa) {
+                     float lr, const SinglesArgs& sa, const PrepArgs* pa) {
     if (T_ == 0 || N == 0) return DLRM_OK;
     T_ <<= ix.vshift;  // virtual tables (row-parity halves) of a forward-launch build
     hipStream_t s = ctx_stream(ctx);
@@ -589,14 +625,22 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
     if (aligned && slots < (1ll << 31)) {
         const int vpr = D * gesz / 16;
         if (tdtype == DLRM_F32 && gdtype == DLRM_F32)
-            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
+            done = dispatch_apply<float, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa, pa);
         else if (tdtype == DLRM_BF16 && gdtype == DLRM_F32)
-            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
+            done = dispatch_apply<uint16_t, float>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa, pa);
         else if (tdtype == DLRM_F32 && gdtype == DLRM_BF16)
-            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa);
+            done = dispatch_apply<float, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N, err, sa, pa);
         else
             done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N,
-                                                      err, sa);
+                                                      err, sa, pa);
+    }
+    if (!done && pa) {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)sizeof(StepLds));
+        (void)attr;
+        hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)(pa->T << pa->ix.vshift)), dim3(256), sizeof(StepLds), s,
+                           *pa);
     }
     if (!done) {
         const int64_t gx0 = (N * D + 255) / 256;

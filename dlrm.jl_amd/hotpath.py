@@ -73,10 +73,16 @@ class HotPath:
         # the training-step pair (dlrm_step_fwd / dlrm_step_bwd): indexer built inside the forward's
         # launch, once-hit rows updated inside the backward's, the rest by the apply launch
         self.step_api = (not self.materialize_ys) and self.indexer is not None and not self.overlap_indexer
-        # pipelined steps (`step_next`): the NEXT batch's split indexer is built on a side stream
-        # during this step, so the step's own launches are the forward (no indexer workgroups),
-        # the backward and the apply; two indexers alternate
-        self.pipeline = bool(pipeline) and self.step_api and self.L == 1
+        # pipelined steps: the NEXT batch's split indexer is built during this step, so the
+        # step's forward launch only gathers; two indexers alternate.
+        #   "apply" (`step_prep`): by extra workgroups of this step's apply launch
+        #           (dlrm_step_bwd_prepare) -- the indexer's latency hides behind the apply's;
+        #   "side"  (`step_next`): by its own launch on a side stream (measured slower: a replayed
+        #           hipGraph runs the side branch serially).
+        mode = {False: None, 0: None, None: None, True: "side", 1: "side", 2: "apply"}.get(pipeline, pipeline)
+        if mode not in (None, "side", "apply"):
+            raise ValueError(f"pipeline must be None, 'side' or 'apply', not {pipeline!r}")
+        self.pipeline = mode if (mode and self.step_api and self.L == 1) else None
         if self.pipeline:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
             self._ix_of = [None, None]  # the PackedIndices each indexer was last built from
@@ -150,12 +156,22 @@ class HotPath:
                                            self.out.stride(0), self.padding))
         self._fwd_x, self._fwd_idx = x, idx
 
-    def step_bwd(self, dout, x=None, idx=None, flags=0):
+    def step_bwd(self, dout, x=None, idx=None, flags=0, prepare=None):
         """dlrm_step_bwd: dot_back + update!(Descent(lr)) with the indexer of step_fwd
         (flags: _lib.STEP_BWD_ONLY / STEP_APPLY_ONLY run one of its two launches)."""
         h = self.ctx.bind()
         x = self._fwd_x if x is None else x
         idx = self._fwd_idx if idx is None else idx
+        if prepare is not None:  # (next indexer, next indices): built by this step's apply launch
+            nix, nidx = prepare
+            if (nidx.itype, nidx.stride, nidx.B, nidx.L) != (idx.itype, idx.stride, idx.B, idx.L):
+                raise ValueError("the next batch's indices must have this batch's layout")
+            self._check(self.lib.dlrm_step_bwd_prepare(h, self.ts.handle, self.indexer.handle, ptr(idx.data),
+                                                       idx.itype, idx.stride, self.index_base, self.B, ptr(x),
+                                                       x.stride(0), ptr(dout), dout.stride(0), self.padding,
+                                                       ptr(self.dx), self.dx.stride(0), ptr(self.dt),
+                                                       self.dt.stride(0), self.lr, nix.handle, ptr(nidx.data), flags))
+            return
         self._check(self.lib.dlrm_step_bwd(h, self.ts.handle, self.indexer.handle, ptr(idx.data), idx.itype,
                                            idx.stride, self.index_base, self.B, ptr(x), x.stride(0), ptr(dout),
                                            dout.stride(0), self.padding, ptr(self.dx), self.dx.stride(0),
@@ -167,10 +183,28 @@ class HotPath:
         self._check(self.lib.dlrm_indexer_build_split(h, indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
                                                       idx.stride, self.index_base, self.B))
 
-    def prime(self, idx):
-        """Builds the indexer of the batch the next `step_next` call will process."""
+    def prime(self, idx, x=None, dout=None, prev=None):
+        """Readies the indexer of the batch the next `step_next` / `step_prep` call will process:
+        "side": builds it; "apply": runs one pipelined step of batch `prev` (x, dout) that
+        prepares `idx` in indexer 0, so the next `step_prep` starts from indexer 0."""
+        if self.pipeline == "apply":
+            self._cur, self._ix_of = 1, [None, None]
+            self.step_prep(x, prev, dout, idx)
+            return
         self.build_split(self._ixs[self._cur], idx)
         self._ix_of[self._cur] = idx
+
+    def step_prep(self, x, idx, dout, next_idx):
+        """One training step of batch `idx` (same math as `step`, bit for bit) whose apply launch
+        also builds batch `next_idx`'s split indexer (dlrm_step_bwd_prepare): when `idx` was
+        prepared by the previous call, this step's forward launch only gathers."""
+        cur, nxt = self._cur, 1 - self._cur
+        self.indexer = self._ixs[cur]
+        self.step_fwd(x, idx)  # gather-only when this indexer holds idx, prepared (the library checks)
+        self.step_bwd(dout, x=x, idx=idx, prepare=(self._ixs[nxt], next_idx))
+        self._ix_of[nxt] = next_idx
+        self._cur = nxt
+        return self.dx
 
     def step_next(self, x, idx, dout, next_idx):
         """One training step of batch `idx` (same math as `step`, bit for bit) that also builds

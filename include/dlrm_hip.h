@@ -283,6 +283,19 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
                   const void* indices, int itype, int64_t table_stride, int index_base, int batch,
                   const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,
                   float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr, unsigned flags);
+/* Pipelined step: dlrm_step_bwd (flags 0) whose apply launch also builds the NEXT batch's split
+ * indexer into next_indexer (same itype / table_stride / index_base / batch as this batch), as
+ * extra workgroups of that launch; the next dlrm_step_fwd with next_indexer and next_indices then
+ * only gathers (one launch without the indexer's workgroups).  Tables and results are identical to
+ * the unpipelined step.  Shapes whose forward has no in-launch indexer (batch > 2048, F > 32, rows
+ * not 16-B aligned) run the plain dlrm_step_bwd and leave next_indexer to the next forward.
+ * next_indices must hold the next batch when the apply runs (stream order).  flags as
+ * dlrm_step_bwd's (the next build rides on the DLRM_STEP_APPLY_ONLY launch). */
+int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
+                          const void* indices, int itype, int64_t table_stride, int index_base, int batch,
+                          const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,
+                          float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, float lr,
+                          dlrm_indexer* next_indexer, const void* next_indices, unsigned flags);
 
 /* ---- table-sharded exchange over RCCL ------------------------------------
  * DLRM.jl is one process: maplookup hands its output straight to the interaction (model.jl:161-163).

@@ -827,13 +827,16 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
         assert np.array_equal(dst.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("mode", ["side", "apply"])
 @pytest.mark.parametrize("rows,D,B,dtype", [("kaggle", 128, 2048, torch.float32),
+                                            ("kaggle", 16, 2048, torch.float32),
                                             ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32),
                                             ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16)])
-def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype):
-    """HotPath.step_next (the next batch's split indexer built on a side stream during the
-    step; eager steps, then hipGraph-captured ones) == the operator sequence over the same
-    batches, bit for bit."""
+def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype, mode):
+    """Pipelined steps (the next batch's split indexer built during the step: "side" =
+    HotPath.step_next on a side stream, "apply" = HotPath.step_prep inside the apply launch, so
+    the next forward only gathers; eager steps, then hipGraph-captured ones) == the operator
+    sequence over the same batches, bit for bit."""
     if rows == "kaggle":
         rows = pkg.KAGGLE_EMBEDDING_SIZES
     rng = np.random.default_rng(B + 7)
@@ -844,18 +847,19 @@ def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype):
     x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
     F = T + 1
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu).to(dtype)
-    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0, pipeline=True)
-    assert hp.pipeline
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0, pipeline=mode)
+    assert hp.pipeline == mode
+    step = hp.step_next if mode == "side" else hp.step_prep
     order = [0, 1, 2, 0]
-    hp.step_next(x, packs[0], dout, packs[1])
-    hp.step_next(x, packs[1], dout, packs[2])
+    step(x, packs[0], dout, packs[1])
+    step(x, packs[1], dout, packs[2])
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            hp.step_next(x, packs[2], dout, packs[0])
-            hp.step_next(x, packs[0], dout, packs[1])
+            step(x, packs[2], dout, packs[0])
+            step(x, packs[0], dout, packs[1])
     torch.cuda.current_stream().wait_stream(s)
     g.replay()
     torch.cuda.synchronize()

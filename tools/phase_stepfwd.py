@@ -26,10 +26,16 @@ x = torch.randn((B, D), device=dev, generator=g)
 for _ in range(5):
     hp.step_fwd(x, p)
 torch.cuda.synchronize()
+lib.dlrm_debug_phase_fwd_reset()
+hp.step_fwd(x, p)
+torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 64)()
 lib.dlrm_debug_phase_fwd.restype = ctypes.c_int
 lib.dlrm_debug_phase_fwd(buf)
 ph = np.array(buf[:64], dtype=np.int64)
-t0 = ph[0] if ph[0] else min(v for v in ph if v)
-print("table", os.environ.get("BLK"), "rows", rows[int(os.environ.get("BLK", "0"))],
-      {k: round((ph[k] - t0) / 100, 2) for k in range(64) if ph[k] >= t0 and ph[k]})
+t0 = min(ph[60], ph[62])  # the launch's first block
+blk = int(os.environ.get("BLK", "0"))
+print(f"block {blk} (table {blk >> hp.indexer_vshift if hasattr(hp, 'indexer_vshift') else blk // 4}):",
+      {k: round((ph[k] - t0) / 100, 2) for k in range(60) if ph[k]},
+      f"| gather blocks {round((ph[60] - t0) / 100, 2)}..{round((ph[61] - t0) / 100, 2)} us,"
+      f" indexer blocks {round((ph[62] - t0) / 100, 2)}..{round((ph[63] - t0) / 100, 2)} us")
