@@ -379,6 +379,8 @@ mutable struct HipTrainStep{T}
     x::Union{Nothing,DeviceMatrix{T}}
     padding::Int
     lr::Float32
+    spare::Union{Nothing,HipIndexer}     # pipelined steps: the indexer the next batch is built into
+    pending::Any                         # (next sparse => its packed indices) after train_step_bwd!(; next)
 end
 function HipTrainStep(ctx::Context, tables::AbstractVector{<:HipEmbedding{Static{D},T}}, batch::Integer;
                       lr = 0.01, pad_to = 1) where {D,T}
@@ -386,12 +388,18 @@ function HipTrainStep(ctx::Context, tables::AbstractVector{<:HipEmbedding{Static
     width, padding = interaction_sizes(D, F, pad_to)
     return HipTrainStep{T}(ctx, collect(tables), HipIndexer(ctx, length(tables), batch),
                            DeviceMatrix{T}(ctx, width, batch), DeviceMatrix{Float32}(ctx, D, batch),
-                           DeviceMatrix{Float32}(ctx, F * D, batch), nothing, nothing, padding, Float32(lr))
+                           DeviceMatrix{Float32}(ctx, F * D, batch), nothing, nothing, padding, Float32(lr),
+                           nothing, nothing)
 end
 
 function train_step_fwd!(st::HipTrainStep{T}, x::AbstractMatrix{T}, sparse) where {T}
     d, B = size(x)
-    st.idx = sparse isa PackedIndices ? sparse : pack(st.ctx, sparse)
+    if st.pending !== nothing && first(st.pending) === sparse
+        st.idx = last(st.pending)        # indexer already built by the previous step's apply
+    else
+        st.idx = sparse isa PackedIndices ? sparse : pack(st.ctx, sparse)
+    end
+    st.pending = nothing
     st.x = x isa DeviceMatrix ? x : upload!(DeviceMatrix{T}(st.ctx, d, B), x)
     check(st.ctx, ccall((:dlrm_step_fwd, libdlrm), Cint,
                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
@@ -401,9 +409,31 @@ function train_step_fwd!(st::HipTrainStep{T}, x::AbstractMatrix{T}, sparse) wher
     return Array(st.out)
 end
 
-function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}) where {T}
+"""
+    train_step_bwd!(st, Δ; next = nothing)
+
+With `next` (the next batch's sparse features) the step's apply launch also builds the next
+batch's indexer (dlrm_step_bwd_prepare), so `train_step_fwd!(st, x_next, next)` only gathers.
+Results are identical either way.
+"""
+function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}; next = nothing) where {T}
     d, B = size(st.x)
     Δd = upload!(DeviceMatrix{T}(st.ctx, size(Δ)...), Matrix{T}(Δ))
+    if next !== nothing
+        nidx = next isa PackedIndices ? next : pack(st.ctx, next)
+        nidx.batch == st.idx.batch || throw(DimensionMismatch("the next batch must have the same size"))
+        nix = st.spare === nothing ? HipIndexer(st.ctx, length(st.tables), B) : st.spare
+        check(st.ctx, ccall((:dlrm_step_bwd_prepare, libdlrm), Cint,
+                            (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid},
+                             Int64, Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat,
+                             Ptr{Cvoid}, Ptr{Cvoid}, Cuint),
+                            st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1,
+                            B, st.x.ptr, d, Δd.ptr, size(Δ, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                            size(st.dt, 1), st.lr, nix.ptr, nidx.data.ptr, Cuint(0)))
+        st.spare, st.ix = st.ix, nix
+        st.pending = next => nidx
+        return Array(st.dx)
+    end
     check(st.ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
                          Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat, Cuint),

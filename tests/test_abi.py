@@ -61,11 +61,10 @@ def test_library_has_gfx950_code_object(pkg):
     assert b"gfx950" in data
 
 
-def test_julia_shim_binds_only_declared_entry_points():
+def test_julia_shim_binds_only_declared_entry_points(pkg):
     """The Julia ccall shim (dlrm.jl_amd/julia/DLRMHip.jl, not executable here: no Julia) names
     only functions the C header declares, so every binding resolves against the library."""
-    import re
-    from dlrm_jl_amd import _lib
+    _lib = pkg._lib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     text = open(os.path.join(root, "dlrm.jl_amd", "julia", "DLRMHip.jl")).read()
     called = set(re.findall(r"ccall\(\(:(dlrm_[a-z0-9_]+)", text))
