@@ -185,7 +185,8 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
 #pragma unroll
                 for (int I = 0; I < NB; ++I) {
                     const bool ok = src[I] && col < d;
-                    const frag v = ldg<frag>((ok ? src[I] : xb) + (ok ? col : 0));
+                    // column steps past d (small d, wave-uniform) issue no load at all
+                    const frag v = u0 + uu * FR::COLS < d ? ldg<frag>((ok ? src[I] : xb) + (ok ? col : 0)) : FR::zero();
                     a[uu][I] = ok ? v : FR::zero();
                 }
             }
