@@ -636,10 +636,13 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
 //  - a once-hit row's old value comes from the gathered rows, moved from the B-operand layout
 //    (lane (c, q): row 4s + q) to the accumulator layout (row 16I + 4q + r) through the wave's
 //    LDS tile, not re-read from HBM.
-// One block = SPB samples (2·SPB waves; grid = ceil(B / SPB)), one pass: both barriers are
+// One block = SPB samples (WPS·SPB waves; grid = ceil(B / SPB)), one pass: both barriers are
 // reached by every wave.  Larger blocks shorten the dispatch ramp (fewer workgroups to place).
-template <typename T, int NB, int DC, int SPB>
-__global__ __launch_bounds__(128 * SPB, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
+// WPS = 1 (d <= 64, one super-block): one wave per sample, the same per-sample load plan --
+// the bwd_body kernel's per-lane index / flag loads (KS + 8 NB instructions before the rows)
+// are most of a small-d backward's time.
+template <typename T, int NB, int DC, int SPB, int WPS = 2>
+__global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
                                                                    int64_t dout_ld, float* __restrict__ dx,
                                                                    int64_t dx_ld, float* __restrict__ dt,
                                                                    int64_t dt_ld, GatherArgs ga,
@@ -650,10 +653,10 @@ __global__ __launch_bounds__(128 * SPB, 4) void interact_bwd_split_kernel(int d_
     constexpr int PMAX = NS * (NS - 1) / 2;
     const int d = DC > 0 ? DC : d_;
     __shared__ float pk_all[SPB][PMAX];  // each sample's packed gradient row
-    __shared__ __attribute__((aligned(16))) float tt_all[2 * SPB][NS * 64];  // each wave's 64-column tile of T
+    __shared__ __attribute__((aligned(16))) float tt_all[WPS * SPB][NS * 64];  // each wave's 64-column tile of T
     __shared__ TableDesc tds[NS];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int pair = w >> 1, h = w & 1;
+    const int pair = w / WPS, h = w % WPS;
     const int c = lane & 15, q = lane >> 4;
     const int64_t b = (int64_t)blockIdx.x * SPB + pair;
     const bool live = b < B;
@@ -669,24 +672,26 @@ __global__ __launch_bounds__(128 * SPB, 4) void interact_bwd_split_kernel(int d_
     const bool tl = lane < F - 1;
     const int64_t myidx = load_index_if(tl, ga.idx, ga.itype, (int64_t)(tl ? lane : 0) * ga.tstride + bb);
     const uint8_t myfl = ldg<uint8_t>(su.single + (tl ? (int64_t)lane * su.cap + bb : 0));
-    float pv[(PMAX + 127) / 128];
+    constexpr int PPW = (PMAX + 64 * WPS - 1) / (64 * WPS);  // packed values staged per lane
+    float pv[PPW];
 #pragma unroll
-    for (int k = 0; k < (PMAX + 127) / 128; ++k) {
-        const int p = h * 64 + lane + 128 * k;
+    for (int k = 0; k < PPW; ++k) {
+        const int p = h * 64 + lane + 64 * WPS * k;
         const float v = to_f32(ldg<T>(ob + d + (p < P ? p : 0)));
         pv[k] = p < P ? v : 0.0f;
     }
-    float xv[DC > 0 ? (DC / 64 + 1) / 2 : 4];
-    constexpr int SBW = DC > 0 ? (DC / 64 + 1) / 2 : 4;  // super-blocks per wave (d <= 512 when not fixed)
+    // super-blocks per wave (WPS = 2: d <= 512 when not fixed; WPS = 1: d <= 64)
+    constexpr int SBW = WPS == 1 ? 1 : (DC > 0 ? (DC / 64 + 1) / 2 : 4);
+    float xv[SBW];
 #pragma unroll
     for (int sbi = 0; sbi < SBW; ++sbi) {
-        const int n = 64 * h + 128 * sbi + lane;
+        const int n = 64 * h + 64 * WPS * sbi + lane;
         xv[sbi] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
     }
     const bool frozen = *su.err != 0;  // a bounds error this step: no table row is written
 #pragma unroll
-    for (int k = 0; k < (PMAX + 127) / 128; ++k) {
-        const int p = h * 64 + lane + 128 * k;
+    for (int k = 0; k < PPW; ++k) {
+        const int p = h * 64 + lane + 64 * WPS * k;
         if (p < PMAX) pk[p] = pv[k];
     }
     __syncthreads();  // tds, pk
@@ -723,7 +728,7 @@ __global__ __launch_bounds__(128 * SPB, 4) void interact_bwd_split_kernel(int d_
     if (h == 0) WT(1, 1, b);
 #pragma unroll
     for (int sbi = 0; sbi < SBW; ++sbi) {
-        const int sb = 64 * h + 128 * sbi;
+        const int sb = 64 * h + 64 * WPS * sbi;
         if (sb >= d) break;
         const int n0 = sb + 4 * c;  // this lane's 4 output columns
         const bool colok = n0 < d;
@@ -1136,7 +1141,7 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     StepUpdate su{ix.single, ix.cap, lr, ctx_error_word(ctx)};
     // one super-block of T rows in flight: two (the gather backward's choice) spill here
     static const int sbu = getenv("DLRM_UPD_SBU") ? atoi(getenv("DLRM_UPD_SBU")) : 1;  // experiment knob
-    // d = 128 (>= two 64-column super-blocks): two waves per sample (interact_bwd_split_kernel)
+    // d = 128 (two 64-column super-blocks): two waves per sample (interact_bwd_split_kernel)
     static const bool split = !getenv("DLRM_BWD_SPLIT") || atoi(getenv("DLRM_BWD_SPLIT")) != 0;
     if (split && d == 128) {
         // samples per block (DLRM_BWD_SPB = 2, 4 or 8 overrides)
@@ -1161,6 +1166,19 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
 #undef DLRM_LAUNCH_SPLIT_S
 #undef DLRM_LAUNCH_SPLIT
         return ctx_hip(ctx, hipGetLastError(), "step_bwd(split) launch");
+    }
+    // d <= 64: the same kernel with one wave per sample, 8 samples per block
+    if (split && d <= 64) {
+#define DLRM_LAUNCH_ONE(TY, N_)                                                                                    \
+    hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 0, 8, 1>), dim3((unsigned)((B + 7) / 8)), dim3(64 * 8), 0, \
+                       s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x, x_ld, su)
+        if (dtype == DLRM_F32) {
+            if (NB == 1) DLRM_LAUNCH_ONE(float, 1); else DLRM_LAUNCH_ONE(float, 2);
+        } else {
+            if (NB == 1) DLRM_LAUNCH_ONE(uint16_t, 1); else DLRM_LAUNCH_ONE(uint16_t, 2);
+        }
+#undef DLRM_LAUNCH_ONE
+        return ctx_hip(ctx, hipGetLastError(), "step_bwd(one wave per sample) launch");
     }
 #define DLRM_LAUNCH_BWDUP(TY, N_)                                                                                  \
     {                                                                                                              \

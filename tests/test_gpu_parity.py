@@ -502,7 +502,10 @@ def _dt_written_mask(idx, D):
     ([50] * 40, 32, 200, None, torch.float32),                         # F = 41: unsplit fallback
     ([50] * 40, 32, 6000, None, torch.float32),                        # F = 41, N > 4096: unsplit hash build
     ([1], 16, 64, None, torch.float32),                                # every position hits one row
-    ([10, 3000, 7, 100000, 3], 256, 512, 1.2, torch.float32)])         # 1-KB rows: 4 chunks per lane group
+    ([10, 3000, 7, 100000, 3], 256, 512, 1.2, torch.float32),          # 1-KB rows: 4 chunks per lane group
+    ([10, 3000, 7, 100000, 3] * 3, 8, 37, 1.1, torch.bfloat16),        # d <= 64: one backward wave per sample
+    ([10, 3000, 7, 100000], 4, 101, None, torch.float32),              # d = 4, partial last block
+    ([30, 500, 7, 20000] * 5, 48, 77, 1.1, torch.float32)])            # d = 48: 3/4 of the super-block
 def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
     """dlrm_step_fwd / dlrm_step_bwd (indexer built in the forward's launch, once-hit rows
     updated inside the backward) == maplookup -> DotInteraction -> dot_back -> update!

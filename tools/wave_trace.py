@@ -17,7 +17,7 @@ pkg = dlrm_pkg.load()
 lib = pkg._lib.load(os.environ["DLRM_HIP_LIB"])
 dev = torch.device("cuda:0")
 rows = pkg.KAGGLE_EMBEDDING_SIZES
-B, D = 2048, 128
+B, D = 2048, int(os.environ.get("DLRM_WT_D", "128"))  # DLRM_WT_D=16: configs[1]
 T = len(rows)
 g = torch.Generator(device=dev).manual_seed(1)
 ts = pkg.EmbeddingTableSet([torch.empty((n, D), device=dev).uniform_(-0.05, 0.05, generator=g) for n in rows])
@@ -36,8 +36,10 @@ def show(kind, slots, names):
     t0 = a[0].min()
     rel = (a - t0) / 100.0  # us
     print(f"  start spread: p50 {np.percentile(rel[0], 50):.2f} p90 {np.percentile(rel[0], 90):.2f} max {rel[0].max():.2f}")
-    for s in range(1, slots):
-        d = rel[s] - rel[s - 1]
+    # slots a launch never writes (e.g. super-block 1 when D <= 64) are skipped
+    used = [s for s in range(slots) if a[s].max() > 0]
+    for prev, s in zip(used, used[1:]):
+        d = rel[s] - rel[prev]
         print(f"  {names[s]:28s} dur p50 {np.percentile(d, 50):.2f} p90 {np.percentile(d, 90):.2f} max {d.max():.2f}"
               f" | done at p50 {np.percentile(rel[s], 50):.2f} max {rel[s].max():.2f}")
 
