@@ -80,15 +80,14 @@ int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what) {
 
 static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device), "hipSetDevice"); }
 
-// parts per table in the step forward's indexer (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides, for
-// comparison)
-static int step_parts_log2() {
-    static const int parts_log2 = [] {
-        const char* e = getenv("DLRM_STEP_PARTS");
-        const int p = e ? atoi(e) : kStepParts;
-        return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
-    }();
-    return parts_log2;
+// parts per table of the step's split indexer build (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides,
+// for comparison).  Measured (profiles/r3m_*): inside the step forward 4 parts (8 add more
+// workgroups than they save in sort depth beside the D = 128 gather); inside the apply launch
+// at small d 8 parts (D = 16: apply + build 12.8 -> 11.4 us), at D = 128 4.
+static int step_parts_log2(int dflt = kStepParts) {
+    static const int forced = getenv("DLRM_STEP_PARTS") ? atoi(getenv("DLRM_STEP_PARTS")) : 0;
+    const int p = forced > 0 ? forced : dflt;
+    return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
 }
 
 static void record_build(dlrm_indexer* ix, bool split, const void* indices, int itype, int64_t tstride, int base,
@@ -889,7 +888,7 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
     next->built = false;
     next->prepared = false;
-    next->dev.vshift = step_parts_log2();
+    next->dev.vshift = step_parts_log2(tb->D <= 32 ? kStepMaxParts : kStepParts);
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
                       next->prep_err};
     rc = step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,
