@@ -525,11 +525,11 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->T = num_tables;
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
     const int64_t T0 = num_tables > 0 ? num_tables : 1;
-    // the forward launch's indexer (batch <= kStepIndexMaxN) sorts each table as up to
-    // kStepMaxParts parts (by the low bits of the row): the per-table arrays then hold that many
-    // virtual tables per table (the hash arrays, single[] and the global sort scratch stay per
-    // real table)
-    const int64_t T = cap <= kStepIndexMaxN ? kStepMaxParts * T0 : T0;
+    // the forward launch's indexer (batch <= kStepIndexMaxN) and the parts build (N <= kPartsMaxN)
+    // sort each table as up to kStepMaxParts parts (by the low bits of the row): the per-table
+    // arrays then hold that many virtual tables per table (the hash arrays, single[] and the
+    // global sort scratch stay per real table)
+    const int64_t T = cap <= kPartsMaxN ? kStepMaxParts * T0 : T0;
     ix->TV = (int)T;
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
@@ -589,6 +589,16 @@ int dlrm_indexer_destroy(dlrm_indexer* ix) {
     return DLRM_OK;
 }
 
+// vshift of a standalone split build of N positions per table: the parts build where it applies
+static int build_vshift(const dlrm_indexer* ix, int64_t N, bool split) {
+    static const int lg = [] {  // DLRM_BUILD_PARTS = 2, 4 or 8 overrides (comparison runs)
+        const char* e = getenv("DLRM_BUILD_PARTS");
+        const int p = e ? atoi(e) : (1 << kPartsLog2);
+        return p >= 8 ? 3 : (p >= 4 ? 2 : 1);
+    }();
+    return split && N > kFastMaxN && N <= kPartsMaxN && ix->TV == kStepMaxParts * ix->T ? lg : 0;
+}
+
 int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, const void* indices, int itype,
                        int64_t table_stride, int index_base, int batch, int lookups) {
     CHECK_ARG(ctx && ix && tb, "dlrm_indexer_build: null argument");
@@ -597,11 +607,11 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_build: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG((int64_t)batch * lookups <= ix->dev.cap, "dlrm_indexer_build: batch*lookups %lld > capacity %lld",
               (long long)batch * lookups, (long long)ix->dev.cap);
-    ix->dev.vshift = 0;
     // the split form where the builds support it: once-hit positions flagged (single[]) instead of
     // listed as one-position chunks; the apply then updates them with no descriptor read
     const int64_t N = (int64_t)batch * lookups;
     const bool split = N <= kFastMaxN || (ix->dev.hsize && N <= kHixMaxN);
+    ix->dev.vshift = build_vshift(ix, N, split);
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups,
                               split);
     if (rc) return rc;
@@ -618,7 +628,7 @@ int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables*
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_build_split: batch %d > capacity %lld", batch,
               (long long)ix->dev.cap);
     ix->built = false;
-    ix->dev.vshift = 0;
+    ix->dev.vshift = build_vshift(ix, batch, true);
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, 1,
                               true, nullptr);
     if (rc) return rc;
@@ -786,16 +796,21 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         }
         if (rc != DLRM_E_UNSUPPORTED) return rc;
     }
-    if (split_ok && ix->dev.hsize && batch > kFastMaxN && batch <= kHixMaxN) {
-        // large batch: the hash build in its split form (once-hit rows left to dlrm_step_bwd), on
-        // the side stream beside the fused forward (launched below); the main stream joins it
+    const int pvs = build_vshift(ix, batch, true);
+    if (split_ok && (pvs > 0 || ix->dev.hsize) && batch > kFastMaxN && batch <= kHixMaxN) {
+        // large batch: the split build (once-hit rows left to dlrm_step_bwd) -- in LDS by table
+        // parts up to kPartsMaxN, else the hash build -- on the side stream beside the fused
+        // forward (launched below); the main stream joins it
         rc = ensure_side(ctx);
         if (rc) return rc;
         rc = ctx_hip(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "hipEventRecord(fork)");
         if (rc == DLRM_OK) rc = ctx_hip(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0), "hipStreamWaitEvent(side)");
+        ix->dev.vshift = pvs;
         if (rc == DLRM_OK)
-            rc = launch_hix_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
-                                  true, ctx->side);
+            rc = pvs > 0 ? launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride,
+                                                index_base, batch, 1, true, ctx->side)
+                         : launch_hix_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base,
+                                            batch, true, ctx->side);
         if (rc == DLRM_OK) rc = ctx_hip(ctx, hipEventRecord(ctx->ev_join, ctx->side), "hipEventRecord(join)");
         if (rc) return rc;
         rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype,

@@ -156,6 +156,14 @@ constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions p
 constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
 constexpr int kStepIndexMaxN = 2048;  // the forward-launch indexer (interact.hip): positions per table
 constexpr int kStepMaxParts = 8;      // ... which sorts a table as up to 8 parts (by the row's low bits)
+// split builds of kFastMaxN < N <= kPartsMaxN positions per table: the in-LDS build (1024
+// threads x 8 positions) over 2^kPartsLog2 parts per table (by the row's low bits), each part's
+// workgroup sized for the worst case (all N positions in one part); larger N: the hash build
+constexpr int kPartsMaxN = 8192;
+#ifndef DLRM_BUILD_PARTS_LOG2
+#define DLRM_BUILD_PARTS_LOG2 2
+#endif
+constexpr int kPartsLog2 = DLRM_BUILD_PARTS_LOG2;
 #ifndef DLRM_STEP_PARTS_DEFAULT
 #define DLRM_STEP_PARTS_DEFAULT 4
 #endif

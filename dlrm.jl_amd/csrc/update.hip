@@ -313,12 +313,12 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
                                                           int base, int N, unsigned* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     FastLds<NT, EPL>& sl = *(FastLds<NT, EPL>*)dyn;
-    const int t = blockIdx.x;
+    const int v = blockIdx.x, t = v >> ix.vshift;  // vshift > 0: one workgroup per table part
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[0][blockIdx.x] = wall_clock64();
 #endif
     PHASE(0);
-    fast_index_table<NT, EPL, SPLIT>(ix, t, t, 0, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
+    fast_index_table<NT, EPL, SPLIT>(ix, v, t, ix.vshift, (uint32_t)tabs[t].nrows, idx, itype, tstride, base, N, err, sl);
 #ifdef DLRM_PHASE
     if (threadIdx.x == 0) g_blk[1][blockIdx.x] = wall_clock64();
 #endif
@@ -522,8 +522,8 @@ static void launch_fast(hipStream_t s, const IndexerDev& ix, const TableDesc* ta
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)sizeof(FastLds<NT, EPL>));
     (void)attr;
-    hipLaunchKernelGGL((indexer_fast_kernel<NT, EPL, SPLIT>), dim3(T_), dim3(NT), sizeof(FastLds<NT, EPL>), s, ix, tabs,
-                       idx, itype, tstride, base, N, err);
+    hipLaunchKernelGGL((indexer_fast_kernel<NT, EPL, SPLIT>), dim3(T_ << ix.vshift), dim3(NT), sizeof(FastLds<NT, EPL>),
+                       s, ix, tabs, idx, itype, tstride, base, N, err);
 }
 
 // split: the form dlrm_step_bwd consumes (once-hit positions flagged, their rows left to the
@@ -535,12 +535,17 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     const int64_t N = (int64_t)B * L;
     unsigned* err = ctx_error_word(ctx);
     static const bool ix256 = getenv("DLRM_IX256") != nullptr;  // experiment knob
-    if (ix256 && N <= 2048 && !split) {  // the 256-thread form the forward / backward launches use, on its own
+    if (ix.vshift > 0) {  // the caller chose the parts build (kFastMaxN < N <= kPartsMaxN, split)
+        if (!split || N > kPartsMaxN)
+            return ctx_fail(ctx, DLRM_E_ARG, "indexer parts build: N=%lld split=%d", (long long)N, (int)split);
+        launch_fast<1024, 8, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
+    } else if (ix256 && N <= 2048 && !split) {  // the 256-thread form the forward / backward launches use, on its own
         launch_fast<256, 8, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
     } else if (N <= 1024 * 2) {
         if (split) launch_fast<1024, 2, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
         else launch_fast<1024, 2, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
-    } else if (N <= kFastMaxN) {  // (8 positions per thread, N <= 8192, measured slower than the hash build)
+    } else if (N <= kFastMaxN) {  // (8 positions per thread, one workgroup per table: slower than the hash
+                                  // build at N = 8192; in 4 parts per table it is the faster one)
         if (split) launch_fast<1024, 4, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
         else launch_fast<1024, 4, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
     } else if (ix.hsize && N <= kHixMaxN) {
