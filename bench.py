@@ -55,10 +55,11 @@ def parse():
                     help="seconds of back-to-back steps timed after the K-step region (reported as 'sustained')")
     ap.add_argument("--pipeline", type=int, default=-1,
                     help="where the step's indexer is built: 0 in the forward's launch; 2 inside the previous "
-                         "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 on a side "
-                         "stream (measured slower: a replayed graph runs the side branch serially); -1 (default): 2 "
-                         "for dim <= 32 (the forward is the indexer's length: D=16 measured 10.9 + 12.7 us vs "
-                         "14.6 + 9.2), else 0 (the gather is the forward's length: D=128 14.0 + 12.9 vs 15.2 + 10.7)")
+                         "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 the next "
+                         "batch's indexer on a side stream during the step; -1 (default): 2 for dim <= 32 (the "
+                         "forward is the indexer's length: D=16 measured 67.1M vs 58.7M samples/s with 0), 1 for "
+                         "one-hot batches > 2048 (no in-launch indexer: configs[2] 73.8M vs 71.7M), else 0 (the "
+                         "gather is the forward's length: D=128 49.0M vs 47.7M with 2)")
     return ap.parse_args()
 
 
@@ -222,7 +223,7 @@ def main():
     w = dict(pkg.WORKLOADS[a.workload])
     B, D, L = w["batch"], w["dim"], w["lookups"]
     if a.pipeline < 0:
-        a.pipeline = 2 if D <= 32 else 0
+        a.pipeline = 2 if D <= 32 else (1 if (L == 1 and B > 2048) else 0)
     if a.mode == "auto":
         a.mode = "eager" if (L > 1 and world == 1) else "graph"
     rows = w["rows"]
