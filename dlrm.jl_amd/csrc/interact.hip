@@ -645,7 +645,9 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
 // WPS = 1 (d <= 64, one super-block): one wave per sample, the same per-sample load plan --
 // the bwd_body kernel's per-lane index / flag loads (KS + 8 NB instructions before the rows)
 // are most of a small-d backward's time.
-template <typename T, int NB, int DC, int SPB, int WPS = 2>
+// MAPPED (dlrm_interact_bwd_blocked): table rows' gradients go to the send layout (GatherArgs dtb /
+// dtl), none to dt's x row; a separate instantiation, so the step kernels keep their LDS budget.
+template <typename T, int NB, int DC, int SPB, int WPS = 2, bool MAPPED = false>
 __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
                                                                    int64_t dout_ld, float* __restrict__ dx,
                                                                    int64_t dx_ld, float* __restrict__ dt,
@@ -659,8 +661,10 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
     __shared__ float pk_all[SPB][PMAX];  // each sample's packed gradient row
     __shared__ __attribute__((aligned(16))) float tt_all[WPS * SPB][NS * 64];  // each wave's 64-column tile of T
     __shared__ TableDesc tds[NS];
+    __shared__ int64_t dmap[MAPPED ? 2 * NS : 1];  // table t's dt rows at dt + dmap[t] + b * dmap[F - 1 + t]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pair = w / WPS, h = w % WPS;
+    constexpr bool mapped = MAPPED;
     const int c = lane & 15, q = lane >> 4;
     const int64_t b = (int64_t)blockIdx.x * SPB + pair;
     const bool live = b < B;
@@ -671,11 +675,18 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
     float* pk = pk_all[pair];
     float* Tt = tt_all[w];
     if (h == 0) WT(1, 0, b);
-    for (int t = threadIdx.x; t < F - 1; t += blockDim.x) tds[t] = load_table(ga.tabs, t);
+    for (int t = threadIdx.x; t < F - 1; t += blockDim.x) {
+        tds[t] = load_table(ga.tabs, t);
+        if constexpr (MAPPED) {
+            dmap[t] = ga.dtb[t];
+            dmap[F - 1 + t] = ga.dtl[t];
+        }
+    }
     // ---- every independent load first: table `lane`'s index and flag, the packed gradients, x part
     const bool tl = lane < F - 1;
     const int64_t myidx = load_index_if(tl, ga.idx, ga.itype, (int64_t)(tl ? lane : 0) * ga.tstride + bb);
-    const uint8_t myfl = ldg<uint8_t>(su.single + (tl ? (int64_t)lane * su.cap + bb : 0));
+    // su.single NULL (dlrm_interact_bwd_blocked): no once-hit update, every table row goes to dt
+    const uint8_t myfl = su.single ? ldg<uint8_t>(su.single + (tl ? (int64_t)lane * su.cap + bb : 0)) : (uint8_t)0;
     constexpr int PPW = (PMAX + 64 * WPS - 1) / (64 * WPS);  // packed values staged per lane
     float pv[PPW];
 #pragma unroll
@@ -788,8 +799,10 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
 #pragma unroll
                         for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
                         store_row<T, 4>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
-                    } else {
+                    } else if constexpr (!mapped) {
                         stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+                    } else if (f > 0) {
+                        stg<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0, v);
                     }
                     if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo + v);
                 }
@@ -1083,6 +1096,27 @@ int launch_interact_bwd_blocked(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_
     GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx), dbase, dld};
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
+    if (L == 1 && NB <= 2 && (d == 128 || d <= 64) && fwd_aligned(dtype, d, x, x_ld, nullptr, 0)) {
+        // the step backward's kernel (two waves per sample at d = 128, one at d <= 64) with no
+        // once-hit update: every table row's gradient goes to the send layout
+        const StepUpdate su{nullptr, 0, 0.0f, ctx_error_word(ctx)};
+#define DLRM_LAUNCH_BLK(TY, N_)                                                                                    \
+    if (d == 128)                                                                                                  \
+        hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 128, 4, 2, true>), dim3((unsigned)((B + 3) / 4)),      \
+                           dim3(128 * 4), 0, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dst, 0, ga, (const TY*)x,\
+                           x_ld, su);                                                                              \
+    else                                                                                                           \
+        hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 0, 2, 1, true>), dim3((unsigned)((B + 1) / 2)),        \
+                           dim3(64 * 2), 0, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dst, 0, ga, (const TY*)x, \
+                           x_ld, su);
+        if (dtype == DLRM_F32) {
+            if (NB == 1) { DLRM_LAUNCH_BLK(float, 1) } else { DLRM_LAUNCH_BLK(float, 2) }
+        } else {
+            if (NB == 1) { DLRM_LAUNCH_BLK(uint16_t, 1) } else { DLRM_LAUNCH_BLK(uint16_t, 2) }
+        }
+#undef DLRM_LAUNCH_BLK
+        return ctx_hip(ctx, hipGetLastError(), "interact_bwd_blocked(split) launch");
+    }
     if (dtype == DLRM_F32)
         dispatch_bwd<float, true>(NB, s, cus, d, F, B, dout, dout_ld, nullptr, 0, dx, dx_ld, dst, 0, ga, x, x_ld);
     else

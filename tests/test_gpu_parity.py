@@ -702,6 +702,10 @@ SHARD_CASES = {
         227605432, 39060, 17295, 7424, 20265, 3, 7122, 1543, 63, 130229467, 3067956, 405282, 10,
         2209, 11938, 155, 4, 976, 14, 292775614, 40790948, 187188510, 590152, 12973, 108, 36]],
         D=32, B=256, L=1, zipf=1.05),
+    # d = 128: the backward's send-layout stores from the two-waves-per-sample kernel
+    "kaggle-scaled-d128": dict(rows=[1460, 583, 10131, 2202, 305, 24, 12517, 633, 3, 9314, 5683, 8351, 3194, 27,
+                                     14992, 5461, 10, 5652, 2173, 4, 7046, 18, 15, 2861, 105, 1425],
+                               D=128, B=128, L=1, zipf=None),
 }
 
 
@@ -765,7 +769,8 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, cas
 
 
 @pytest.mark.parametrize("owners,graphed,case", [(None, False, "small"), ([[4, 0, 2], [1, 3]], True, "small"),
-                                                 ("fitting", True, "terabyte-scaled")])
+                                                 ("fitting", True, "terabyte-scaled"),
+                                                 (None, True, "kaggle-scaled-d128")])
 def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed, case):
     """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange; contiguous,
     explicit or TablePartition.fitting's byte-balanced non-contiguous assignment; eager or
