@@ -322,7 +322,7 @@ def main():
 
     if a.mode == "graph":
         try:
-            for piece in set(plan(a.steps)) | set(plan(nb)):
+            for piece in set(plan(a.steps)) | set(plan(nb)) | set(plan(a.warmup)):
                 if piece not in graphs:
                     graphs[piece] = capture(*piece)
             torch.cuda.synchronize()
@@ -342,6 +342,11 @@ def main():
             graphs[piece].replay()
 
     def timed(n):
+        # the W untimed warm-up steps run right before the region (the first warm-up pass above sits
+        # behind graph capture and host work, which leave the GPU idle), then the pipelined indexer
+        # is re-primed for batch 0
+        if a.warmup > 0:
+            run_steps(a.warmup)
         prime()  # (outside the timed region)
         if world > 1:
             dist.barrier()
