@@ -56,8 +56,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=-1,
                     help="where the step's indexer is built: 0 in the forward's launch; 2 inside the previous "
                          "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 the next "
-                         "batch's indexer on a side stream during the step; -1 (default): 2 for dim <= 32 (the "
-                         "forward is the indexer's length: D=16 measured 67.1M vs 58.7M samples/s with 0), 1 for "
+                         "batch's indexer on a side stream during the step; -1 (default): 2 for rows of <= 256 B "
+                         "(the forward is the indexer's length: D=16 measured 67.1M vs 58.7M samples/s with 0, "
+                         "Terabyte bf16 x 128 45.6M vs 41.9M), 1 for "
                          "one-hot batches > 2048 (no in-launch indexer: configs[2] 73.8M vs 71.7M), else 0 (the "
                          "gather is the forward's length: D=128 49.0M vs 47.7M with 2)")
     return ap.parse_args()
@@ -222,13 +223,16 @@ def main():
             dist.init_process_group(backend)
     w = dict(pkg.WORKLOADS[a.workload])
     B, D, L = w["batch"], w["dim"], w["lookups"]
+    E = 4 if w["dtype"] == "f32" else 2
     if a.pipeline < 0:
-        a.pipeline = 2 if D <= 32 else (1 if (L == 1 and B > 2048) else 0)
+        # in-apply build where the forward's gather is shorter than its in-launch indexer: rows of
+        # <= 256 B (D=16 fp32; Terabyte bf16 x 128: 45.6M vs 41.9M samples/s, profiles/r5c_*)
+        small_rows = D <= 32 or (D * E <= 256 and L == 1 and B <= 2048)
+        a.pipeline = 2 if small_rows else (1 if (L == 1 and B > 2048) else 0)
     if a.mode == "auto":
         a.mode = "eager" if (L > 1 and world == 1) else "graph"
     rows = w["rows"]
     T = len(rows)
-    E = 4 if w["dtype"] == "f32" else 2
     nb = a.nbatch
 
     if world == 1:

@@ -83,7 +83,7 @@ static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device
 // parts per table of the step's split indexer build (DLRM_STEP_PARTS = 1, 2, 4 or 8 overrides,
 // for comparison).  Measured (profiles/r3m_*): inside the step forward 4 parts (8 add more
 // workgroups than they save in sort depth beside the D = 128 gather); inside the apply launch
-// at small d 8 parts (D = 16: apply + build 12.8 -> 11.4 us), at D = 128 4.
+// for rows of <= 256 B 8 parts (D = 16: apply + build 12.8 -> 11.4 us), for fp32 x 128 4.
 static int step_parts_log2(int dflt = kStepParts) {
     static const int forced = getenv("DLRM_STEP_PARTS") ? atoi(getenv("DLRM_STEP_PARTS")) : 0;
     const int p = forced > 0 ? forced : dflt;
@@ -903,7 +903,10 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
     next->built = false;
     next->prepared = false;
-    next->dev.vshift = step_parts_log2(tb->D <= 32 ? kStepMaxParts : kStepParts);
+    // 8 parts where the apply's rows are <= 256 B (D = 16 fp32; Terabyte bf16 x 128: 47.8M vs 45.2M
+    // samples/s with 4, profiles/r5d_*), 4 for the 512-B fp32 x 128 rows
+    const int row_bytes = tb->D * (tb->dtype == DLRM_F32 ? 4 : 2);
+    next->dev.vshift = step_parts_log2(row_bytes <= 256 ? kStepMaxParts : kStepParts);
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
                       next->prep_err};
     rc = step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,

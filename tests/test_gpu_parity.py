@@ -839,7 +839,11 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
 @pytest.mark.parametrize("rows,D,B,dtype", [("kaggle", 128, 2048, torch.float32),
                                             ("kaggle", 16, 2048, torch.float32),
                                             ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32),
-                                            ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16)])
+                                            ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16),
+                                            # Terabyte-shaped bf16 x 128 at B = 2048: the in-apply
+                                            # build runs 8 parts per table (256-B rows)
+                                            ([3, 200000, 60, 50000, 10, 100000] * 4 + [7, 30000], 128, 2048,
+                                             torch.bfloat16)])
 def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype, mode):
     """Pipelined steps (the next batch's split indexer built during the step: "side" =
     HotPath.step_next on a side stream, "apply" = HotPath.step_prep inside the apply launch, so
