@@ -302,6 +302,7 @@ def main():
     prime()
 
     def capture(start, n):
+        prime()  # every piece is captured from the state it is replayed in (indexer primed for batch 0)
         cur = torch.cuda.current_stream()
         s = torch.cuda.Stream()
         s.wait_stream(cur)
@@ -349,7 +350,10 @@ def main():
         # the W untimed warm-up steps run right before the region (the first warm-up pass above sits
         # behind graph capture and host work, which leave the GPU idle), then the pipelined indexer
         # is re-primed for batch 0
+        # (pipelined graphs are valid only from the state they were captured in: every replayed
+        # piece starts at batch 0, so the indexer is re-primed before each run)
         if a.warmup > 0:
+            prime()
             run_steps(a.warmup)
         prime()  # (outside the timed region)
         if world > 1:

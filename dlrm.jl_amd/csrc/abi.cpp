@@ -48,6 +48,7 @@ struct dlrm_indexer {
     bool built = false;
     bool split = false;  // built by dlrm_step_fwd's kernel: once-hit rows are left to the backward
     bool prepared = false;  // built by dlrm_step_bwd_prepare for the next dlrm_step_fwd (not yet consumed)
+    bool singles_done = false;  // a split backward has applied this build's once-hit rows already
     unsigned* prep_err = nullptr;  // device word: bounds errors of a prepared build (the forward re-raises)
     const void* indices = nullptr;
     int itype = 0, base = 0, B = 0, L = 0;
@@ -58,6 +59,7 @@ namespace dlrm {
 unsigned* ctx_error_word(dlrm_ctx* ctx) { return ctx->err; }
 hipStream_t ctx_stream(dlrm_ctx* ctx) { return ctx->stream; }
 int ctx_num_cus(dlrm_ctx* ctx) { return ctx->cus; }
+int ctx_device(dlrm_ctx* ctx) { return ctx->device; }
 int ctx_fail(dlrm_ctx* ctx, int code, const char* fmt, ...) {
     if (ctx) {
         va_list ap;
@@ -95,6 +97,7 @@ static void record_build(dlrm_indexer* ix, bool split, const void* indices, int 
     ix->built = true;
     ix->split = split;
     ix->prepared = false;
+    ix->singles_done = false;
     ix->indices = indices;
     ix->itype = itype;
     ix->tstride = tstride;
@@ -742,9 +745,10 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, unsigned f
     rc = ensure_partials(ctx, ix, tb->D);
     if (rc) return rc;
     // a split indexer (dlrm_indexer_build's default form, or dlrm_step_fwd's): its once-hit
-    // positions are this launch's too
-    const SinglesArgs sa{ix->split ? ix->dev.single : nullptr, indices, itype, table_stride, index_base,
-                         batch * lookups};
+    // positions are this launch's too -- unless a split backward (dlrm_step_bwd) has updated them
+    // already, in which case only the repeated rows are left (their dt rows are all it wrote)
+    const SinglesArgs sa{(ix->split && !ix->singles_done) ? ix->dev.single : nullptr, indices, itype, table_stride,
+                         index_base, batch * lookups};
     return launch_sgd_apply(ctx, ix->dev, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, lookups,
                             (int64_t)batch * lookups, grad, grad_dtype, grad_ld, grad_offset, lr, sa);
 }
@@ -861,6 +865,7 @@ static int step_bwd_impl(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const
                   "dlrm_step_bwd: dx and dt must be 16-B aligned with leading dimensions divisible by 4");
         rc = launch_step_bwd(ctx, tb->d_desc, tb->T, tb->dtype, indices, itype, table_stride, index_base, d, batch, x,
                              x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, ix->dev, lr);
+        if (rc == DLRM_OK) ix->singles_done = true;
     } else {
         rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                         index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, nullptr);
@@ -893,8 +898,10 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     // the next batch's build runs as extra workgroups of this step's apply launch: the step
     // forward's split build (the same parts), so the next dlrm_step_fwd only gathers
     const int NB = (tb->T + 1 + 15) / 16;
+    // (the split backward's shapes only: the apply launch that carries the build has no once-hit items)
     const bool inapply = batch > 0 && tb->T > 0 && batch <= kStepIndexMaxN && NB <= 2 && tb->aligned16 &&
-                         next->TV == kStepMaxParts * next->T;
+                         next->TV == kStepMaxParts * next->T &&
+                         step_split_supported(tb->aligned16, tb->T, tb->dtype, tb->D, x, x_ld);
     if (!inapply)  // no pipelined form for this shape: the plain step (the next forward builds)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);

@@ -40,6 +40,9 @@ int nccl_fail(dlrm_ctx* ctx, ncclResult_t r, const char* what) {
 int exchange(dlrm_ctx* ctx, dlrm_comm* comm, ncclDataType_t dt, size_t esize, const void* send, void* recv,
              const std::vector<size_t>& soff, const std::vector<size_t>& scount, const std::vector<size_t>& roff,
              const std::vector<size_t>& rcount, const char* what) {
+    if (dlrm::ctx_device(ctx) != comm->device)
+        return dlrm::ctx_fail(ctx, DLRM_E_ARG, "%s: ctx is on device %d, the communicator on device %d", what,
+                              dlrm::ctx_device(ctx), comm->device);
     hipStream_t s = dlrm::ctx_stream(ctx);
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return nccl_fail(ctx, r, what);
@@ -72,8 +75,13 @@ int dlrm_comm_init(dlrm_ctx* ctx, const void* id, int rank, int nranks, dlrm_com
     *out = nullptr;
     dlrm_comm* c = new (std::nothrow) dlrm_comm();
     if (!c) return DLRM_E_NOMEM;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    // the communicator lives on the ctx's device, whatever device the calling thread has current
+    const int dev = dlrm::ctx_device(ctx);
+    const hipError_t he = hipSetDevice(dev);
+    if (he != hipSuccess) {
+        delete c;
+        return dlrm::ctx_hip(ctx, he, "dlrm_comm_init: hipSetDevice");
+    }
     c->rank = rank;
     c->nranks = nranks;
     c->device = dev;

@@ -212,6 +212,7 @@ hipStream_t ctx_stream(dlrm_ctx* ctx);
 int ctx_fail(dlrm_ctx* ctx, int code, const char* fmt, ...);
 int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what);
 int ctx_num_cus(dlrm_ctx* ctx);
+int ctx_device(dlrm_ctx* ctx);
 
 int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                      const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,

@@ -128,11 +128,174 @@ struct GatherArgs {
     const int64_t* dtl;
 };
 
+// A zero row: the source of padding rows (16NB > F) and of rows whose index is out of range, so
+// that every row load of the one-hot forward is an unconditional, unmasked load.
+constexpr int kZeroElems = 1024;  // fp32 elements (4 KB); column offsets wrap modulo this
+__device__ __attribute__((aligned(16))) float g_zero_row[kZeroElems];
+
+// One-hot forward (L = 1): every row load of a column block (all UU x NB fragments) is issued
+// before the first MFMA, so a wave keeps its whole sample's rows in flight at once.  The
+// compiler's own schedule interleaved one load, a wait and its MFMAs (one 1-KB load in flight per
+// wave: the row stream ran at 2 TB/s); the sched_barriers pin the order
+//   index / table loads | row loads | x staging + MFMAs.
+// Row 0 of T is x itself: it arrives with the rows, and the output's x head (fast_vcat) is
+// staged from those fragments instead of a second load of x.
+template <typename T, int NB, bool FUSED, int WPB, int DC = 0>
+__device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* stage_all, int d_, int F, int B,
+                                                const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys,
+                                                int64_t ys_ld, T* __restrict__ out, int64_t out_ld, int padding,
+                                                const GatherArgs& ga) {
+    const int d = DC > 0 ? DC : d_;
+    typedef Frag<T> FR;
+    typedef typename FR::type frag;
+    constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 15, q = lane >> 4;
+    const int P = F * (F - 1) / 2;
+    const int W = d + P + padding;
+    const bool staged = W <= kStage;
+    float* stage = stage_all + w * kStage;
+    const T* zero = (const T*)g_zero_row;
+    constexpr int ZMASK = kZeroElems * 4 / (int)sizeof(T) - 1;
+    for (int64_t b = (int64_t)bid * WPB + w; b < B; b += (int64_t)nblocks * WPB) {
+        WT(0, 0, b);
+        const T* xb = x + b * x_ld;
+        T* yb = ys ? ys + b * ys_ld : nullptr;
+        T* orow = out + b * out_ld;
+        const T* src[NB];
+        if (FUSED) {
+            // every index and descriptor load first (one round trip), then the checks
+            TableDesc td[NB];
+            int64_t ri[NB];
+#pragma unroll
+            for (int I = 0; I < NB; ++I) {
+                const int row = I * 16 + c;
+                const bool tab = row >= 1 && row < F;
+                td[I] = load_table(ga.tabs, tab ? row - 1 : 0);
+                ri[I] = load_index_if(tab, ga.idx, ga.itype, tab ? (row - 1) * ga.tstride + b : 0);
+            }
+            bool bad = false;
+#pragma unroll
+            for (int I = 0; I < NB; ++I) {
+                const int row = I * 16 + c;
+                const bool tab = row >= 1 && row < F;
+                const int64_t r = ri[I] - ga.base;
+                const bool ok = tab & (r >= 0) & (r < td[I].nrows);
+                bad |= tab & !ok;
+                src[I] = row == 0 ? xb : (ok ? (const T*)td[I].data + r * d : nullptr);
+            }
+            if (bad & (q == 0)) raise_index_error(ga.err);
+        } else {
+#pragma unroll
+            for (int I = 0; I < NB; ++I) {
+                const int row = I * 16 + c;
+                src[I] = row == 0 ? xb : (row < F ? yb + (int64_t)row * d : nullptr);
+            }
+        }
+        f32x4_t acc[NB * (NB + 1) / 2];
+#pragma unroll
+        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int u0 = 0; u0 < d; u0 += UU * FR::COLS) {
+            __builtin_amdgcn_sched_barrier(0);
+            frag a[UU][NB];
+#pragma unroll
+            for (int uu = 0; uu < UU; ++uu) {
+                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
+                // column steps wholly past d (small d; wave-uniform) issue no load
+                if (DC > 0 ? (uu * FR::COLS < DC) : (u0 + uu * FR::COLS < d)) {
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) {
+                        const bool ok = src[I] && col < d;
+                        a[uu][I] = ldg<frag>(ok ? src[I] + col : zero + (col & ZMASK));
+                    }
+                } else {
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) a[uu][I] = FR::zero();
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int uu = 0; uu < UU; ++uu) {
+                int ij = 0;
+#pragma unroll
+                for (int I = 0; I < NB; ++I)
+#pragma unroll
+                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[ij], a[uu][I], a[uu][J]);
+            }
+            // fast_vcat: x (row 0: lanes c == 0 of I = 0) into the output head, and the lookup
+            // output ys rows (FUSED with ys kept), from the fragments (after the MFMAs, so the MFMAs
+            // wait for their own loads only)
+#pragma unroll
+            for (int uu = 0; uu < UU; ++uu) {
+                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
+                if (col < d) {
+                    if (c == 0) {
+                        float f[FR::PER_LANE];
+                        FR::to_f(f, a[uu][0]);
+                        if (staged) {
+#pragma unroll
+                            for (int k = 0; k < FR::PER_LANE; k += 4)
+                                *(f32x4_t*)(stage + col + k) = f32x4_t{f[k], f[k + 1], f[k + 2], f[k + 3]};
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < FR::PER_LANE; ++k) stg<T>(orow + col + k, from_f32<T>(f[k]));
+                        }
+                        if (yb) stg<frag>(yb + col, a[uu][0]);
+                    }
+                    if (FUSED && yb) {
+#pragma unroll
+                        for (int I = 0; I < NB; ++I) {
+                            const int row = I * 16 + c;
+                            if (row >= 1 && row < F) stg<frag>(yb + (int64_t)row * d + col, a[uu][I]);
+                        }
+                    }
+                }
+            }
+        }
+        WT(0, 1, b);
+        // Z[i][j], i > j: triangular_slice_kernel! order (i-major), after x
+        {
+            int ij = 0;
+#pragma unroll
+            for (int I = 0; I < NB; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J, ++ij) {
+                    const int j = J * 16 + c;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = I * 16 + 4 * q + r;
+                        if (i < F && j < i) {
+                            const int e = d + i * (i - 1) / 2 + j;
+                            if (staged) stage[e] = acc[ij][r];
+                            else stg<T>(orow + e, from_f32<T>(acc[ij][r]));
+                        }
+                    }
+                }
+        }
+        for (int e = d + P + lane; e < W; e += 64) {
+            if (staged) stage[e] = 0.0f;
+            else stg<T>(orow + e, from_f32<T>(0.0f));
+        }
+        if (staged) {
+            wave_lds_sync();
+            for (int e = lane; e < W; e += 64) stg<T>(orow + e, from_f32<T>(stage[e]));
+            wave_lds_sync();
+        }
+        WT(0, 2, b);
+    }
+}
+
 // Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
 template <typename T, int NB, bool FUSED, int WPB, bool POOL = false, int DC = 0>
 __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all, int d_, int F, int B,
                                          const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                          T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga) {
+    // !POOL: one lookup per (table, sample) -- the callers pick the POOL kernel for FUSED, L > 1
+    if constexpr (!POOL) {
+        fwd_body_onehot<T, NB, FUSED, WPB, DC>(bid, nblocks, stage_all, d_, F, B, x, x_ld, ys, ys_ld, out, out_ld,
+                                               padding, ga);
+        return;
+    }
     const int d = DC > 0 ? DC : d_;  // DC: the feature size as a compile-time constant
     typedef Frag<T> FR;
     typedef typename FR::type frag;
@@ -281,7 +444,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F,
                                                                    int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                                                    T* __restrict__ out, int64_t out_ld, int padding,
                                                                    GatherArgs ga) {
-    __shared__ float stage_all[WPB * kStage];
+    __shared__ __attribute__((aligned(16))) float stage_all[WPB * kStage];
     fwd_body<T, NB, FUSED, WPB, POOL, DC>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding,
                                 ga);
 }
@@ -675,12 +838,14 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
     float* pk = pk_all[pair];
     float* Tt = tt_all[w];
     if (h == 0) WT(1, 0, b);
-    for (int t = threadIdx.x; t < F - 1; t += blockDim.x) {
-        tds[t] = load_table(ga.tabs, t);
-        if constexpr (MAPPED) {
-            dmap[t] = ga.dtb[t];
-            dmap[F - 1 + t] = ga.dtl[t];
-        }
+    // the table descriptors (F - 1 <= NS <= 32 < blockDim: one per thread), held in registers and
+    // written to LDS after the other independent loads are issued, so no wave waits for them alone
+    const bool tdl_ok = (int)threadIdx.x < F - 1;
+    const TableDesc tdl = load_table(ga.tabs, tdl_ok ? (int)threadIdx.x : 0);
+    int64_t dm0 = 0, dm1 = 0;
+    if constexpr (MAPPED) {
+        dm0 = ldg<int64_t>(ga.dtb + (tdl_ok ? threadIdx.x : 0));
+        dm1 = ldg<int64_t>(ga.dtl + (tdl_ok ? threadIdx.x : 0));
     }
     // ---- every independent load first: table `lane`'s index and flag, the packed gradients, x part
     const bool tl = lane < F - 1;
@@ -704,6 +869,13 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
         xv[sbi] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
     }
     const bool frozen = *su.err != 0;  // a bounds error this step: no table row is written
+    if (tdl_ok) {
+        tds[threadIdx.x] = tdl;
+        if constexpr (MAPPED) {
+            dmap[threadIdx.x] = dm0;
+            dmap[F - 1 + threadIdx.x] = dm1;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
         const int p = h * 64 + lane + 64 * WPS * k;

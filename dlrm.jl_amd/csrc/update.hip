@@ -411,6 +411,14 @@ __global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
                                                pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err, *(StepLds*)lds);
 }
 
+// step_index_kernel's own launch (the next batch's split build when the apply launch cannot carry it)
+static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StepLds));
+    (void)attr;
+    hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)(pa.T << pa.ix.vshift)), dim3(256), sizeof(StepLds), s, pa);
+}
+
 // Generic (any D) versions: one thread per element column.
 template <typename TT, typename GT>
 __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,
@@ -583,7 +591,7 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     if (grid < 1) grid = 1;
     // (the once-hit items and the next batch's indexer are separate instantiations: the step's
     // apply stays lean)
-    if (pa) {
+    if (pa && !sa.single) {
         static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                                            (int)sizeof(StepLds));
@@ -595,6 +603,8 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     } else if (sa.single) {
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 1>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
                            tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});
+        // MODE 2 has no once-hit items: the next batch's build (if any) gets its own launch
+        if (pa) launch_step_index(s, *pa);
     } else {
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 0>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
                            tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});
@@ -639,14 +649,7 @@ int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool 
             done = dispatch_apply<uint16_t, uint16_t>(vpr, s, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, N,
                                                       err, sa, pa);
     }
-    if (!done && pa) {
-        static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           (int)sizeof(StepLds));
-        (void)attr;
-        hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)(pa->T << pa->ix.vshift)), dim3(256), sizeof(StepLds), s,
-                           *pa);
-    }
+    if (!done && pa) launch_step_index(s, *pa);
     if (!done) {
         const int64_t gx0 = (N * D + 255) / 256;
         const unsigned gx = (unsigned)(gx0 < 1 ? 1 : (gx0 > 4096 ? 4096 : gx0));

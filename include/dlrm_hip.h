@@ -265,7 +265,10 @@ int dlrm_sgd_update(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer, u
  *   where the shape allows (F <= 32, batch <= 2048): the indexer's workgroups sort while the
  *   gather streams.  `out` is bit-identical to dlrm_lookup_interact_fwd's.  The indexer is
  *   built in "split" form: rows hit by exactly one position of the batch are flagged for the
- *   backward instead of listed for the apply (dlrm_sgd_update refuses such an indexer).
+ *   backward instead of listed for the apply.  dlrm_sgd_update(PREBUILT) with such an indexer
+ *   updates the flagged rows too -- unless dlrm_step_bwd's backward (DLRM_STEP_BWD_ONLY or flags 0)
+ *   already has, in which case it updates only the repeated rows from their dt rows, so every row
+ *   is stepped exactly once whichever call follows the backward.
  * dlrm_step_bwd = dlrm_interact_bwd_gather + dlrm_sgd_update(Descent(lr), PREBUILT) with that
  *   indexer.  dx is bit-identical to dlrm_interact_bwd_gather's and the tables end up
  *   bit-identical to dlrm_sgd_update's result: a once-hit row gets w = fmaf(-lr, g, w) inside
@@ -290,7 +293,10 @@ int dlrm_step_bwd(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
  * the unpipelined step.  Shapes whose forward has no in-launch indexer (batch > 2048, F > 32, rows
  * not 16-B aligned) run the plain dlrm_step_bwd and leave next_indexer to the next forward.
  * next_indices must hold the next batch when the apply runs (stream order).  flags as
- * dlrm_step_bwd's (the next build rides on the DLRM_STEP_APPLY_ONLY launch). */
+ * dlrm_step_bwd's (the next build rides on the DLRM_STEP_APPLY_ONLY launch).
+ * Whether dlrm_step_fwd only gathers is decided on the host when it is called (the indexer holds
+ * these indices, prepared): a hipGraph captured from a pipelined sequence is valid only when it is
+ * replayed from the indexer state it was captured in (e.g. re-prime before each replayed run). */
 int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tables, dlrm_indexer* indexer,
                           const void* indices, int itype, int64_t table_stride, int index_base, int batch,
                           const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, int padding,

@@ -542,6 +542,71 @@ def test_step_api_matches_operator_sequence(pkg, gpu, rows, D, B, zipf, dtype):
         assert np.array_equal(to_np_bits(a.data), to_np_bits(b.data))
 
 
+def _operator_steps(pkg, tabs, gpu, dtype, D, p, x, dout, lr, nsteps):
+    """The reference's operator sequence (maplookup -> DotInteraction -> dot_back -> update!)."""
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype))
+    for _ in range(nsteps):
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, p, index_base=0)
+        out, back = pkg.rrule(pkg.DotInteraction(), x, ys)
+        _, dx, dy = back(dout)
+        pkg.update_(pkg.Descent(lr), ts, pkg.maplookup_pullback(D, ts, p, dy), index_base=0)
+    return ts, out, dx
+
+
+def test_split_backward_then_prebuilt_update_steps_each_row_once(pkg, gpu):
+    """dlrm_step_bwd(BWD_ONLY) updates the once-hit rows itself; a following
+    dlrm_sgd_update(PREBUILT) with the same split indexer must then apply only the repeated rows
+    (it stepped the once-hit rows a second time from dt rows never written)."""
+    rows, D, B = [3, 40, 100000, 7, 2_000_000], 128, 512
+    rng = np.random.default_rng(11)
+    tabs = rand_tables(rng, rows, D)
+    idx_np = rand_indices(rng, rows, B, 1)
+    p = pkg.PackedIndices(torch.from_numpy(idx_np).to(torch.int32).to(gpu))
+    x = torch.randn((B, D), device=gpu)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.5, index_base=0)
+    dout = torch.randn((B, hp.width), device=gpu)
+    hp.dt.fill_(float("nan"))  # once-hit rows' dt entries stay unwritten: reading one poisons the table
+    hp.step_fwd(x, p)
+    hp.step_bwd(dout, x=x, idx=p, flags=pkg._lib.STEP_BWD_ONLY)
+    hp.sgd_update(p, prebuilt=True)
+    torch.cuda.synchronize()
+    ts_ref, out, dx = _operator_steps(pkg, tabs, gpu, torch.float32, D, p, x, dout, 0.5, 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_f32(hp.dx), to_np_f32(dx))
+    for a, b in zip(hp.ts, ts_ref):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+
+
+def test_prepare_with_unaligned_x_updates_once_hit_rows(pkg, gpu):
+    """dlrm_step_bwd_prepare after dlrm_indexer_build_split with an x whose rows are not 16-B
+    aligned (no split backward for it, so the apply must take the once-hit rows too): every row is
+    stepped (the apply launch that carried the next build had no once-hit items; such
+    shapes now take the plain step and leave the next build to the next forward)."""
+    rows, D, B = [5, 300, 100000, 9, 1_000_000], 16, 256
+    rng = np.random.default_rng(12)
+    tabs = rand_tables(rng, rows, D)
+    batches = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+               for _ in range(2)]
+    xs = torch.randn((B, D + 1), device=gpu)
+    x = xs[:, 1:]  # row stride D + 1: not 16-B aligned
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0)
+    dout = torch.randn((B, hp.width), device=gpu)
+    nxt = pkg.SparseIndexer(len(rows), B, gpu)
+    hp.build_split(hp.indexer, batches[0])
+    hp.step_bwd(dout, x=x, idx=batches[0], prepare=(nxt, batches[1]))
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    ts = pkg.EmbeddingTableSet(dev_tables(tabs, gpu))
+    ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, batches[0], index_base=0)
+    _, back = pkg.rrule(pkg.DotInteraction(), x.contiguous(), ys)
+    _, dx, dy = back(dout)
+    pkg.update_(pkg.Descent(0.25), ts, pkg.maplookup_pullback(D, ts, batches[0], dy), index_base=0)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(to_np_f32(hp.dx), to_np_f32(dx), rtol=1e-5, atol=1e-6)
+    for a, b in zip(hp.ts, ts):
+        np.testing.assert_allclose(to_np_f32(a.data), to_np_f32(b.data), rtol=1e-5, atol=1e-6)
+
+
 def test_step_api_state_and_bounds(pkg, gpu):
     """The forward's split indexer also drives the plain update (once-hit rows included, bit for
     bit the update of a fresh build); step_bwd needs step_fwd's indices; an out-of-range index
