@@ -38,6 +38,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="kaggle-d128-b2048")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: the global batch (split evenly over the ranks; e.g. configs[3]: "
+                         "--workload terabyte-d128-zipf --global-batch 2048 = 256 per GPU at 8 GPUs); 0 (default): "
+                         "weak scaling, the workload's batch per GPU")
+    ap.add_argument("--micro", type=int, default=0,
+                    help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
+                         "0: the engine's default (2 where a rank's batch is >= 256)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -193,13 +200,16 @@ def cpu_baseline(pkg, w, seconds, threads):
                       f"reference (no julia toolchain)"}
 
 
-def load_pmc(workload, kernel):
+def load_prof(workload):
+    """The committed rocprofv3 summary of this workload (tools/profile.sh -> profiles/pmc_<workload>.json:
+    per-stage rocprof average durations, PMC HBM bytes and MFMA busy fractions, with the HEAD it was
+    taken at), or None."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+            return json.load(f)
     except Exception:
         return None
 
@@ -222,13 +232,17 @@ def main():
         else:
             dist.init_process_group(backend)
     w = dict(pkg.WORKLOADS[a.workload])
+    if a.global_batch:
+        if a.global_batch % world:
+            raise SystemExit(f"--global-batch {a.global_batch} does not split over {world} ranks")
+        w["batch"] = a.global_batch // world
     B, D, L = w["batch"], w["dim"], w["lookups"]
     E = 4 if w["dtype"] == "f32" else 2
     if a.pipeline < 0:
         # in-apply build where the forward's gather is shorter than its in-launch indexer: rows of
-        # <= 256 B (D=16 fp32; Terabyte bf16 x 128: 45.6M vs 41.9M samples/s, profiles/r5c_*)
-        small_rows = D <= 32 or (D * E <= 256 and L == 1 and B <= 2048)
-        a.pipeline = 2 if small_rows else (1 if (L == 1 and B > 2048) else 0)
+        # <= 256 B (D=16 fp32; Terabyte bf16 x 128: 45.6M vs 41.9M samples/s, profiles/r5c_*);
+        # the same choice tests/test_configs.py checks against the oracle (shapes.step_pipeline)
+        a.pipeline = {None: 0, "side": 1, "apply": 2}[pkg.step_pipeline(w)]
     if a.mode == "auto":
         a.mode = "eager" if (L > 1 and world == 1) else "graph"
     rows = w["rows"]
@@ -262,7 +276,8 @@ def main():
                 engine.step(x, packs[k % nb], dout)
     else:
         from dlrm_jl_amd.sharded import make_bench_engine
-        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb)
+        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb,
+                                                         micro=a.micro or None)
         if a.mode == "graph":
             # the compute between the two all-to-alls is replayed as hipGraphs; the collectives
             # are launched eagerly (RCCL inside hipGraph capture: not relied on)
@@ -504,14 +519,33 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / (reps * nb)
             stages[n] = {"us": round(us, 2), "alg_bytes": int(bytes_[n]),
                          "GBps": round(bytes_[n] / (us * 1e-6) / 1e9, 1)}
-        # the dominant kernel of the step's critical path (a side-stream stage overlaps it)
-        dom = max((n for n in names if not (engine.pipeline == "side" and n == "indexer_build")),
-                  key=lambda n: stages[n]["us"])
+        for n in names:
+            stages[n]["frac"] = round(stages[n]["GBps"] / HBM_PEAK_GBS, 4)
+        # the dominant kernel of the step's critical path (a side-stream stage overlaps it): the
+        # longest launch in the committed rocprofv3 summary of this workload when it has every stage
+        # (the same kernels, timed by the profiler), else by the HIP-event timings above
+        crit = [n for n in names if not (engine.pipeline == "side" and n == "indexer_build")]
+        prof = load_prof(a.workload)
+        have = prof is not None and all(n in prof and "avg_us" in prof[n] for n in crit)
+        dom = max(crit, key=lambda n: prof[n]["avg_us"] if have else stages[n]["us"])
         ach = stages[dom]["GBps"]
+        step_bytes = sum(bytes_[n] for n in names)  # every launch of one step (side-stream work included)
+        step_gbs = step_bytes / (ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc(a.workload, dom),
+                    "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": (prof or {}).get(dom, {}).get("hbm_bytes_per_launch"),
                     "alg_bytes_per_launch": int(bytes_[dom]), "avg_launch_us": stages[dom]["us"],
+                    "step": {"alg_bytes": int(step_bytes), "ms": round(ms, 4), "GBps": round(step_gbs, 1),
+                             "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
                     "stages": stages}
+        if prof is not None:
+            roofline["profile"] = {"file": f"profiles/pmc_{a.workload}.json", "head": prof.get("head"),
+                                   "dominant_by": "rocprofv3 avg duration" if have else "HIP events",
+                                   "rocprof_avg_us": {n: round(prof[n]["avg_us"], 2) for n in names
+                                                      if n in prof and "avg_us" in prof[n]}}
+            mf = {n: round(prof[n]["mfma_busy"], 4) for n in names if n in prof and "mfma_busy" in prof[n]}
+            if mf:  # north_star: MFMA utilisation of the interaction kernels (SIMD-cycle fraction)
+                roofline["mfma"] = mf
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and w["dtype"] == "f32":
@@ -528,7 +562,8 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "strong" if a.global_batch else "weak",
             "vs_baseline": None, "dtype": w["dtype"],
             "data": (f"synthetic ({'Zipf(%g) over permuted rows' % w['zipf'] if w.get('zipf') else 'uniform'} "
                      "indices, ScaledUniform tables, N(0,1) x, N(0,1e-3) dLoss/dout)"),
@@ -538,6 +573,7 @@ def main():
                                        + ("RCCL all-to-all" if dist.get_backend() == "nccl" else
                                           f"{dist.get_backend()} all-to-all (host-staged rehearsal)")),
                        "index_batches": nb,
+                       **({"micro_batches": engine.M} if world > 1 else {}),
                        "launch": (f"hipGraph replay (<= {chunk} steps per graph)" if graphs is not None else
                                   "hipGraph replay of the compute between eager all-to-alls" if a.mode == "segments"
                                   else "eager"),

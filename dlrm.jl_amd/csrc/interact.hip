@@ -55,235 +55,9 @@ extern "C" int dlrm_debug_wtrace(unsigned long long* out) {
 #define WT(kind, slot, b) do {} while (0)
 #endif
 
+#include "fwd_onehot.hpp"
+
 namespace dlrm {
-
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-
-constexpr int kStage = 1024;  // floats of output staging per wave
-
-// ---------------------------------------------------------------------------------- fwd
-// Fragment traits: fp32 -> v_mfma_f32_16x16x4_f32 with float4 loads (16 columns per step, 4
-// MFMA k-steps, one per component); bf16 -> v_mfma_f32_16x16x32_bf16 with 8-element loads
-// (32 columns per step, one MFMA).
-template <typename T> struct Frag;
-template <> struct Frag<float> {
-    typedef f32x4_t type;
-    static constexpr int COLS = 16, PER_LANE = 4;
-    __device__ static inline type zero() { return type{0.f, 0.f, 0.f, 0.f}; }
-    __device__ static inline void mma(f32x4_t& acc, const type& a, const type& b) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], b[k], acc, 0, 0, 0);
-    }
-    __device__ static inline void add_to(float* f, const type& v) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] += v[k];
-    }
-    __device__ static inline void to_f(float* f, const type& v) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = v[k];
-    }
-    __device__ static inline type from_f(const float* f) { return type{f[0], f[1], f[2], f[3]}; }
-};
-template <> struct Frag<uint16_t> {
-    typedef bf16x8_t type;
-    static constexpr int COLS = 32, PER_LANE = 8;
-    __device__ static inline type zero() { return type{}; }
-    __device__ static inline void mma(f32x4_t& acc, const type& a, const type& b) {
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-    }
-    __device__ static inline void to_f(float* f, const type& v) {
-        const u16x8 u = __builtin_bit_cast(u16x8, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] = bf16_to_f32(u[k]);
-    }
-    __device__ static inline void add_to(float* f, const type& v) {
-        float g[8];
-        to_f(g, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] += g[k];
-    }
-    __device__ static inline type from_f(const float* f) {
-        u16x8 u;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) u[k] = f32_to_bf16(f[k]);
-        return __builtin_bit_cast(type, u);
-    }
-};
-
-// Where the embedding rows come from: the ys buffer (the reference's two-operator form), or
-// straight from the tables (maplookup fused into the interaction: every gathered row is read
-// once into MFMA fragments and written to ys from registers — ys is never read back).
-struct GatherArgs {
-    const TableDesc* tabs;
-    const void* idx;
-    int itype;
-    int64_t tstride;
-    int base;
-    int L;
-    unsigned* err;
-    // backward: when set, table t's dt row of sample b goes to dt + dtb[t] + b * dtl[t] (device
-    // arrays; the sharded exchange's per-owner send layout) and dt's x row is not written
-    const int64_t* dtb;
-    const int64_t* dtl;
-};
-
-// A zero row: the source of padding rows (16NB > F) and of rows whose index is out of range, so
-// that every row load of the one-hot forward is an unconditional, unmasked load.
-constexpr int kZeroElems = 1024;  // fp32 elements (4 KB); column offsets wrap modulo this
-__device__ __attribute__((aligned(16))) float g_zero_row[kZeroElems];
-
-// One-hot forward (L = 1): every row load of a column block (all UU x NB fragments) is issued
-// before the first MFMA, so a wave keeps its whole sample's rows in flight at once.  The
-// compiler's own schedule interleaved one load, a wait and its MFMAs (one 1-KB load in flight per
-// wave: the row stream ran at 2 TB/s); the sched_barriers pin the order
-//   index / table loads | row loads | x staging + MFMAs.
-// Row 0 of T is x itself: it arrives with the rows, and the output's x head (fast_vcat) is
-// staged from those fragments instead of a second load of x.
-template <typename T, int NB, bool FUSED, int WPB, int DC = 0>
-__device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* stage_all, int d_, int F, int B,
-                                                const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys,
-                                                int64_t ys_ld, T* __restrict__ out, int64_t out_ld, int padding,
-                                                const GatherArgs& ga) {
-    const int d = DC > 0 ? DC : d_;
-    typedef Frag<T> FR;
-    typedef typename FR::type frag;
-    constexpr int UU = 128 / FR::COLS;  // column steps whose loads are issued together (128 columns)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 15, q = lane >> 4;
-    const int P = F * (F - 1) / 2;
-    const int W = d + P + padding;
-    const bool staged = W <= kStage;
-    float* stage = stage_all + w * kStage;
-    const T* zero = (const T*)g_zero_row;
-    constexpr int ZMASK = kZeroElems * 4 / (int)sizeof(T) - 1;
-    for (int64_t b = (int64_t)bid * WPB + w; b < B; b += (int64_t)nblocks * WPB) {
-        WT(0, 0, b);
-        const T* xb = x + b * x_ld;
-        T* yb = ys ? ys + b * ys_ld : nullptr;
-        T* orow = out + b * out_ld;
-        const T* src[NB];
-        if (FUSED) {
-            // every index and descriptor load first (one round trip), then the checks
-            TableDesc td[NB];
-            int64_t ri[NB];
-#pragma unroll
-            for (int I = 0; I < NB; ++I) {
-                const int row = I * 16 + c;
-                const bool tab = row >= 1 && row < F;
-                td[I] = load_table(ga.tabs, tab ? row - 1 : 0);
-                ri[I] = load_index_if(tab, ga.idx, ga.itype, tab ? (row - 1) * ga.tstride + b : 0);
-            }
-            bool bad = false;
-#pragma unroll
-            for (int I = 0; I < NB; ++I) {
-                const int row = I * 16 + c;
-                const bool tab = row >= 1 && row < F;
-                const int64_t r = ri[I] - ga.base;
-                const bool ok = tab & (r >= 0) & (r < td[I].nrows);
-                bad |= tab & !ok;
-                src[I] = row == 0 ? xb : (ok ? (const T*)td[I].data + r * d : nullptr);
-            }
-            if (bad & (q == 0)) raise_index_error(ga.err);
-        } else {
-#pragma unroll
-            for (int I = 0; I < NB; ++I) {
-                const int row = I * 16 + c;
-                src[I] = row == 0 ? xb : (row < F ? yb + (int64_t)row * d : nullptr);
-            }
-        }
-        f32x4_t acc[NB * (NB + 1) / 2];
-#pragma unroll
-        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        for (int u0 = 0; u0 < d; u0 += UU * FR::COLS) {
-            __builtin_amdgcn_sched_barrier(0);
-            frag a[UU][NB];
-#pragma unroll
-            for (int uu = 0; uu < UU; ++uu) {
-                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
-                // column steps wholly past d (small d; wave-uniform) issue no load
-                if (DC > 0 ? (uu * FR::COLS < DC) : (u0 + uu * FR::COLS < d)) {
-#pragma unroll
-                    for (int I = 0; I < NB; ++I) {
-                        const bool ok = src[I] && col < d;
-                        a[uu][I] = ldg<frag>(ok ? src[I] + col : zero + (col & ZMASK));
-                    }
-                } else {
-#pragma unroll
-                    for (int I = 0; I < NB; ++I) a[uu][I] = FR::zero();
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int uu = 0; uu < UU; ++uu) {
-                int ij = 0;
-#pragma unroll
-                for (int I = 0; I < NB; ++I)
-#pragma unroll
-                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[ij], a[uu][I], a[uu][J]);
-            }
-            // fast_vcat: x (row 0: lanes c == 0 of I = 0) into the output head, and the lookup
-            // output ys rows (FUSED with ys kept), from the fragments (after the MFMAs, so the MFMAs
-            // wait for their own loads only)
-#pragma unroll
-            for (int uu = 0; uu < UU; ++uu) {
-                const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
-                if (col < d) {
-                    if (c == 0) {
-                        float f[FR::PER_LANE];
-                        FR::to_f(f, a[uu][0]);
-                        if (staged) {
-#pragma unroll
-                            for (int k = 0; k < FR::PER_LANE; k += 4)
-                                *(f32x4_t*)(stage + col + k) = f32x4_t{f[k], f[k + 1], f[k + 2], f[k + 3]};
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < FR::PER_LANE; ++k) stg<T>(orow + col + k, from_f32<T>(f[k]));
-                        }
-                        if (yb) stg<frag>(yb + col, a[uu][0]);
-                    }
-                    if (FUSED && yb) {
-#pragma unroll
-                        for (int I = 0; I < NB; ++I) {
-                            const int row = I * 16 + c;
-                            if (row >= 1 && row < F) stg<frag>(yb + (int64_t)row * d + col, a[uu][I]);
-                        }
-                    }
-                }
-            }
-        }
-        WT(0, 1, b);
-        // Z[i][j], i > j: triangular_slice_kernel! order (i-major), after x
-        {
-            int ij = 0;
-#pragma unroll
-            for (int I = 0; I < NB; ++I)
-#pragma unroll
-                for (int J = 0; J <= I; ++J, ++ij) {
-                    const int j = J * 16 + c;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = I * 16 + 4 * q + r;
-                        if (i < F && j < i) {
-                            const int e = d + i * (i - 1) / 2 + j;
-                            if (staged) stage[e] = acc[ij][r];
-                            else stg<T>(orow + e, from_f32<T>(acc[ij][r]));
-                        }
-                    }
-                }
-        }
-        for (int e = d + P + lane; e < W; e += 64) {
-            if (staged) stage[e] = 0.0f;
-            else stg<T>(orow + e, from_f32<T>(0.0f));
-        }
-        if (staged) {
-            wave_lds_sync();
-            for (int e = lane; e < W; e += 64) stg<T>(orow + e, from_f32<T>(stage[e]));
-            wave_lds_sync();
-        }
-        WT(0, 2, b);
-    }
-}
 
 // Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
 template <typename T, int NB, bool FUSED, int WPB, bool POOL = false, int DC = 0>
@@ -292,8 +66,10 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
                                          T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga) {
     // !POOL: one lookup per (table, sample) -- the callers pick the POOL kernel for FUSED, L > 1
     if constexpr (!POOL) {
-        fwd_body_onehot<T, NB, FUSED, WPB, DC>(bid, nblocks, stage_all, d_, F, B, x, x_ld, ys, ys_ld, out, out_ld,
-                                               padding, ga);
+        // two waves per sample at the BASELINE feature size (d = 128: 4 fp32 / 2 bf16 column steps each)
+        constexpr int WPS = (DC == 128 && NB <= 2 && WPB % 2 == 0) ? 2 : 1;
+        fwd_body_onehot<T, NB, FUSED, WPB, DC, WPS>(bid, nblocks, stage_all, d_, F, B, x, x_ld, ys, ys_ld, out,
+                                                    out_ld, padding, ga);
         return;
     }
     const int d = DC > 0 ? DC : d_;  // DC: the feature size as a compile-time constant
@@ -337,9 +113,9 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
                               : (!FUSED ? (row < F ? yb + (int64_t)row * d : nullptr)
                                         : (ok ? (const T*)td[I].data + r * d : nullptr));
         }
-        f32x4_t acc[NB * (NB + 1) / 2];
+        f32x4_t acc2[NB <= 2 ? 2 : 1][NB * (NB + 1) / 2];  // NB <= 2: parity partials (fwd_body_onehot's order)
 #pragma unroll
-        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc2[0][k] = acc2[NB <= 2 ? 1 : 0][k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         for (int u0 = 0; u0 < d; u0 += UU * FR::COLS) {
             frag a[UU][NB];
 #pragma unroll
@@ -402,9 +178,12 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
 #pragma unroll
                 for (int I = 0; I < NB; ++I)
 #pragma unroll
-                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[ij], a[uu][I], a[uu][J]);
+                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc2[NB <= 2 ? (uu & 1) : 0][ij], a[uu][I], a[uu][J]);
             }
         }
+        f32x4_t acc[NB * (NB + 1) / 2];
+#pragma unroll
+        for (int k = 0; k < NB * (NB + 1) / 2; ++k) acc[k] = NB <= 2 ? acc2[0][k] + acc2[1][k] : acc2[0][k];
         WT(0, 1, b);
         // Z[i][j], i > j: triangular_slice_kernel! order (i-major), after x
         {
@@ -970,11 +749,11 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
                         const f32x4_t tw = *(const f32x4_t*)(Tt + f * 64 + 4 * c);  // the row as gathered
 #pragma unroll
                         for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
-                        store_row<T, 4>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
+                        store_row<T, 4, true>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
                     } else if constexpr (!mapped) {
-                        stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+                        stg_nt<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
                     } else if (f > 0) {
-                        stg<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0, v);
+                        stg_nt<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0, v);
                     }
                     if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo + v);
                 }
@@ -1062,10 +841,14 @@ static unsigned grid_for(int64_t items, int per_block, int cus) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
+// samples per 4-wave workgroup of the one-hot forward: two waves per sample at d = 128 (NB <= 2)
+static int fwd_samples_per_block(int d, int NB) { return (d == 128 && NB <= 2) ? 2 : 4; }
+
 template <typename T, int NB, bool FUSED>
 static void launch_fwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
                           int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
-    const unsigned g = grid_for(B, 4, cus);
+    const bool pooled = FUSED && ga.L > 1;
+    const unsigned g = grid_for(B, pooled ? 4 : fwd_samples_per_block(d, NB), cus);
     if (FUSED && ga.L > 1)
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, true>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
                            x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
@@ -1318,7 +1101,7 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
     size_t lds = sizeof(StepLds);
     if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
-    const unsigned g = grid_for(B, 4, cus) + (T_ << ix.vshift);
+    const unsigned g = grid_for(B, fwd_samples_per_block(d, NB), cus) + (T_ << ix.vshift);
 #define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
     if (d == 128)                                                                                                  \
         hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_, 128>), dim3(g), dim3(256), lds, s, d, F, B,            \

@@ -157,6 +157,16 @@ class PackedIndices:
         self.data = data.contiguous()
         self.T, self.B, self.L = int(T), int(B), int(L)
 
+    @classmethod
+    def columns(cls, packed, b0, b1):
+        """Samples [b0, b1) of every table as a view (no copy): data [T][(b1-b0)*L] with the
+        parent's table stride (the micro-batch slices of the sharded step)."""
+        v = cls.__new__(cls)
+        L = packed.L
+        v.data = packed.data[:, b0 * L:b1 * L]
+        v.T, v.B, v.L = packed.T, int(b1 - b0), L
+        return v
+
     def on(self, device):
         """This index set on `device` (self if already there)."""
         return self if self.data.device == torch.device(device) else PackedIndices(self, device=device)

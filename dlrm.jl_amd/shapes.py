@@ -39,6 +39,17 @@ WORKLOADS = {
 }
 
 
+def step_pipeline(w):
+    """Where the training step's split indexer is built for workload `w` (the form bench.py times
+    and tests/test_configs.py checks against the oracle): "apply" = inside the previous step's apply
+    launch (rows of <= 256 B, batches <= 2048: the forward then only gathers), "side" = the next
+    batch's build on a side stream (one-hot batches > 2048), None = inside the forward's launch."""
+    E = 4 if w["dtype"] == "f32" else 2
+    D, L, B = w["dim"], w["lookups"], w["batch"]
+    small_rows = D <= 32 or (D * E <= 256 and L == 1 and B <= 2048)
+    return "apply" if small_rows else ("side" if (L == 1 and B > 2048) else None)
+
+
 def table_bytes(rows, dim, esize):
     return sum(rows) * dim * esize
 

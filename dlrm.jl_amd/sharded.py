@@ -4,8 +4,14 @@ The reference has no distributed code; this is the MI355X extens
 north star asks for: embedding tables shard BY TABLE across ranks, and one all-to-all each
 way moves the looked-up vectors to the ranks that own the samples, and their gradients back.
 
-  rank r owns the tables tables(r) (a TablePartition) and samples [r*B, (r+1)*B) of the
-  global batch Bg = world * B (weak scaling: B per GPU is fixed).
+  rank r owns the tables tables(r) (a TablePartition) and B samples of the global batch
+  Bg = world * B (weak scaling: B per GPU fixed; strong scaling: Bg fixed, B = Bg / world).
+  The step runs as M micro-batches of Bm = B / M samples per rank, so the all-to-all of one
+  micro-batch overlaps the compute of the next on a second stream.  Micro-batch m of the global
+  batch is its samples [m*world*Bm, (m+1)*world*Bm), in rank order: rank r's local sample b is
+  global sample  global_index(r, b) = (b // Bm) * world * Bm + r * Bm + b % Bm
+  (M = 1: r * B + b), so each micro-batch's index columns, exchange blocks and gradient rows are
+  contiguous, and the update sees the global batch in global order.
 
   forward : maplookup of r's T_r tables for all Bg samples, written straight into the
             exchange layout (dlrm_maplookup_blocked)        -> send [world][T_r][B][D]
@@ -22,6 +28,11 @@ way moves the looked-up vectors to the ranks that own the samples, and their gra
             SparseIndexer (positions grouped by row: a hash build over the whole chip for
             Bg*L > 4096) depends on the indices only and is built on a side stream while
             the forward runs
+
+Per rank and step: lookup(m) for every m on the compute stream; exchange_fwd(m) on the comm stream
+as soon as lookup(m) is done; interaction fwd + bwd of m once its vectors arrived; exchange_bwd(m) on
+the comm stream; the update when the last gradient block arrived.  Exposed: the first forward and
+the last backward exchange (1/M of each direction) -- DESIGN.md §6.
 
 All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-ABI kernels)
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
@@ -115,12 +126,13 @@ class HipShardOps:
         if rc != _lib.OK:
             self.ctx.check(rc)
 
-    def bind_recv(self, tabs):
-        """tabs: the T received [B][D] blocks in global table order (views of one buffer)."""
-        self.rts = EmbeddingTableSet(tabs)
-        T, B = len(tabs), tabs[0].shape[0]
-        ar = torch.arange(B, dtype=torch.int32, device=self.device)
-        self.ident = PackedIndices(ar.repeat(T, 1).reshape(T, B, 1))
+    def bind_recv(self, tabs_per_mb):
+        """tabs_per_mb[m]: micro-batch m's T received [Bm][D] blocks in global table order (views of
+        its receive buffer); each block is a Bm-row table read in place with identity indices."""
+        self.rts = [EmbeddingTableSet(tabs) for tabs in tabs_per_mb]
+        T, Bm = len(tabs_per_mb[0]), tabs_per_mb[0][0].shape[0]
+        ar = torch.arange(Bm, dtype=torch.int32, device=self.device)
+        self.ident = PackedIndices(ar.repeat(T, 1).reshape(T, Bm, 1))
 
     def build_indexer(self, idx):
         self._ok(self.lib.dlrm_indexer_build(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
@@ -135,27 +147,27 @@ class HipShardOps:
         self._ok(self.lib.dlrm_scatter_rows(self.ctx.bind(), src.element_size(), T, B, D, ptr(src), src_ld, src_off,
                                             ptr(dst), ptr(dbase), ptr(dld)))
 
-    def interact_fwd_recv(self, x, out, padding):
+    def interact_fwd_recv(self, x, out, padding, m=0):
         i = self.ident
-        self._ok(self.lib.dlrm_lookup_interact_fwd(self.ctx.bind(), self.rts.handle, ptr(i.data), i.itype, i.stride,
-                                                   0, i.B, 1, ptr(x), x.stride(0), None, 0, ptr(out), out.stride(0),
-                                                   padding))
+        self._ok(self.lib.dlrm_lookup_interact_fwd(self.ctx.bind(), self.rts[m].handle, ptr(i.data), i.itype,
+                                                   i.stride, 0, i.B, 1, ptr(x), x.stride(0), None, 0, ptr(out),
+                                                   out.stride(0), padding))
 
-    def interact_bwd_recv(self, dout, x, dx, dt, padding):
+    def interact_bwd_recv(self, dout, x, dx, dt, padding, m=0):
         i = self.ident
-        self._ok(self.lib.dlrm_interact_bwd_gather(self.ctx.bind(), self.rts.handle, None, ptr(i.data), i.itype,
+        self._ok(self.lib.dlrm_interact_bwd_gather(self.ctx.bind(), self.rts[m].handle, None, ptr(i.data), i.itype,
                                                    i.stride, 0, i.B, 1, ptr(x), x.stride(0), ptr(dout),
                                                    dout.stride(0), padding, ptr(dx), dx.stride(0), ptr(dt),
                                                    dt.stride(0)))
 
-    def interact_bwd_send(self, dout, x, dx, gsend, dbase, dld, padding):
-        """dot_back on the received tables with every table's dt rows stored straight into the
-        exchange's send layout (one launch: dlrm_interact_bwd_blocked).  False: shape not
+    def interact_bwd_send(self, dout, x, dx, gsend, dbase, dld, padding, m=0):
+        """dot_back on micro-batch m's received tables with every table's dt rows stored straight
+        into the exchange's send layout (one launch: dlrm_interact_bwd_blocked).  False: shape not
         supported by the fused kernel (the caller repacks dt instead)."""
         i = self.ident
-        rc = self.lib.dlrm_interact_bwd_blocked(self.ctx.bind(), self.rts.handle, ptr(i.data), i.itype, i.stride, 0,
-                                                i.B, ptr(x), x.stride(0), ptr(dout), dout.stride(0), padding, ptr(dx),
-                                                dx.stride(0), ptr(gsend), ptr(dbase), ptr(dld))
+        rc = self.lib.dlrm_interact_bwd_blocked(self.ctx.bind(), self.rts[m].handle, ptr(i.data), i.itype, i.stride,
+                                                0, i.B, ptr(x), x.stride(0), ptr(dout), dout.stride(0), padding,
+                                                ptr(dx), dx.stride(0), ptr(gsend), ptr(dbase), ptr(dld))
         if rc == _lib.E_UNSUPPORTED:
             return False
         self._ok(rc)
@@ -172,12 +184,18 @@ class HipShardOps:
 
 
 class ShardedHotPath:
-    """One step of the table-sharded hot path on this rank (see module docstring)."""
+    """One step of the table-sharded hot path on this rank, as `micro` micro-batches (see the
+    module docstring)."""
 
-    def __init__(self, ops, partition, rank, batch_local, dim, lookups, dtype, device, group=None, exchange=None):
+    def __init__(self, ops, partition, rank, batch_local, dim, lookups, dtype, device, group=None, exchange=None,
+                 micro=1):
         self.ops, self.part, self.rank = ops, partition, rank
         self.world = partition.world
         self.B, self.D, self.L = batch_local, dim, lookups
+        if micro < 1 or batch_local % micro:
+            raise ValueError(f"{micro} micro-batches do not divide {batch_local} samples per rank")
+        self.M = micro
+        self.Bm = batch_local // micro
         self.Bg = batch_local * self.world
         self.T = partition.T
         self.F = self.T + 1
@@ -186,29 +204,32 @@ class ShardedHotPath:
         self.group = group
         _, self.width, self.padding = interaction_sizes(dim, self.F)
         dev = device
-        D, B, T, Tr, W = dim, batch_local, self.T, self.Tr, self.world
-        self.send = torch.empty((W * Tr * B * D,), dtype=dtype, device=dev)
-        self.recv = torch.empty((T * B * D,), dtype=dtype, device=dev)
+        D, B, Bm, T, Tr, W, M = dim, batch_local, self.Bm, self.T, self.Tr, self.world, micro
+        # per micro-batch exchange buffers (forward: send [peer][T_r][Bm][D] -> recv [src][T_j][Bm][D];
+        # backward: gsend [owner][Bm][T_j][D] -> rows [m*W*Bm, (m+1)*W*Bm) of grad [Bg][T_r*D])
+        self.send = torch.empty((M, W * Tr * Bm * D), dtype=dtype, device=dev)
+        self.recv = torch.empty((M, T * Bm * D), dtype=dtype, device=dev)
         self.out = torch.empty((B, self.width), dtype=dtype, device=dev)
         self.dx = torch.empty((B, D), dtype=torch.float32, device=dev)
-        self.dt = None  # [B][F*D] fp32, only where the backward cannot store into gsend directly
-        self.gsend = torch.empty((T * B * D,), dtype=torch.float32, device=dev)
+        self.dt = None  # [Bm][F*D] fp32, only where the backward cannot store into gsend directly
+        self.gsend = torch.empty((M, T * Bm * D), dtype=torch.float32, device=dev)
         self.grecv = torch.empty((W * Tr * B * D,), dtype=torch.float32, device=dev)
         self.grad = self.grecv.view(self.Bg, Tr * D) if Tr else None
-        # element counts of each peer's block (flat all_to_all_single splits)
-        self.fwd_in_splits = [Tr * B * D] * W
-        self.fwd_out_splits = [c * B * D for c in partition.counts]
+        # element counts of each peer's block (flat all_to_all_single splits), per micro-batch
+        self.fwd_in_splits = [Tr * Bm * D] * W
+        self.fwd_out_splits = [c * Bm * D for c in partition.counts]
         self.bwd_in_splits = self.fwd_out_splits
         self.bwd_out_splits = self.fwd_in_splits
         # received block of global table t: position of t in the exchange order
         slot = {t: i for i, t in enumerate(partition.order)}
-        self.recv_tables = [self.recv[slot[t] * B * D:(slot[t] + 1) * B * D].view(B, D) for t in range(T)]
-        # gsend block of owner j = [B][T_j][D]: table t (k-th of its owner) at base + b * T_j * D
+        self.recv_tables = [[self.recv[m, slot[t] * Bm * D:(slot[t] + 1) * Bm * D].view(Bm, D) for t in range(T)]
+                            for m in range(M)]
+        # gsend block of owner j = [Bm][T_j][D]: table t (k-th of its owner) at base + b * T_j * D
         base, ld, off = [0] * T, [0] * T, 0
         for j, tabs in enumerate(partition.owners):
             for k, t in enumerate(tabs):
                 base[t], ld[t] = off + k * D, len(tabs) * D
-            off += len(tabs) * B * D
+            off += len(tabs) * Bm * D
         self.gs_base = torch.tensor(base, dtype=torch.int64, device=dev)
         self.gs_ld = torch.tensor(ld, dtype=torch.int64, device=dev)
         ops.bind_recv(self.recv_tables)
@@ -224,7 +245,19 @@ class ShardedHotPath:
             raise ValueError(f"exchange must be 'torch' or 'abi', not {exchange!r}")
         self._graphs = None
         self._fused_bwd = None  # None: not tried yet; False: the ops cannot (repack instead)
-        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        cuda = dev.type == "cuda"
+        self._side = torch.cuda.Stream(device=dev) if cuda else None   # the indexer build
+        self._cstream = torch.cuda.Stream(device=dev) if cuda else None  # the exchanges
+        self._ev = ([[torch.cuda.Event() for _ in range(M)] for _ in range(4)] if cuda else None)
+        self._ix_done = torch.cuda.Event() if cuda else None
+
+    def global_index(self, b, rank=None):
+        """The global-batch sample of local sample b (this rank, or `rank`)."""
+        r = self.rank if rank is None else rank
+        return (b // self.Bm) * self.world * self.Bm + r * self.Bm + b % self.Bm
+
+    def rows(self, m):
+        return slice(m * self.Bm, (m + 1) * self.Bm)
 
     # ---- exchange (pure data movement; identical for every ShardOps)
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -237,52 +270,60 @@ class ShardedHotPath:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def exchange_fwd(self):
+    def grad_rows(self, m):
+        """Micro-batch m's gradient rows of grad [Bg][T_r*D] (flat)."""
+        n = self.world * self.Bm * self.Tr * self.D
+        return self.grecv[m * n:(m + 1) * n]
+
+    def exchange_fwd(self, m=0):
         if self.comm is not None:
-            self.comm.alltoall_fwd(self.send, self.recv, self.D, self.B, self.part.counts)
+            self.comm.alltoall_fwd(self.send[m], self.recv[m], self.D, self.Bm, self.part.counts)
             return
-        self._a2a(self.recv, self.send, self.fwd_out_splits, self.fwd_in_splits)
+        self._a2a(self.recv[m], self.send[m], self.fwd_out_splits, self.fwd_in_splits)
 
-    def pack_grad(self):
-        """dt's table columns -> gsend [owner j][B][T_j][D] (one launch)."""
-        self.ops.scatter_rows(self.dt, self.F * self.D, self.D, self.gsend, self.gs_base, self.gs_ld, self.T, self.B,
-                              self.D)
+    def pack_grad(self, m=0):
+        """dt's table columns -> gsend[m] [owner j][Bm][T_j][D] (one launch)."""
+        self.ops.scatter_rows(self.dt, self.F * self.D, self.D, self.gsend[m], self.gs_base, self.gs_ld, self.T,
+                              self.Bm, self.D)
 
-    def exchange_bwd(self):
+    def exchange_bwd(self, m=0):
         if self.comm is not None:
-            self.comm.alltoall_bwd(self.gsend, self.grecv, self.D, self.B, self.part.counts)
+            self.comm.alltoall_bwd(self.gsend[m], self.grad_rows(m), self.D, self.Bm, self.part.counts)
             return
-        self._a2a(self.grecv, self.gsend, self.bwd_out_splits, self.bwd_in_splits)
+        self._a2a(self.grad_rows(m), self.gsend[m], self.bwd_out_splits, self.bwd_in_splits)
 
-    # ---- the step, as three compute segments around the two exchanges
+    # ---- the step's compute segments
     def seg_index(self, idx):
         """The update's SparseIndexer (depends on the indices only)."""
         if self.Tr:
             self.ops.build_indexer(idx)
 
-    def seg_lookup(self, idx):
-        """idx: PackedIndices of this rank's tables for the GLOBAL batch ([T_r][Bg*L]);
-        the gathered vectors land in the exchange layout send [world][T_r][B][D]."""
+    def seg_lookup(self, idx, m=0):
+        """idx: PackedIndices of this rank's tables for the GLOBAL batch ([T_r][Bg*L], global order);
+        micro-batch m's columns are gathered into its exchange layout send[m] [world][T_r][Bm][D]."""
         if self.Tr:
-            B, D, Tr = self.B, self.D, self.Tr
-            self.ops.lookup_blocked(idx, self.send, D, B * D, B, Tr * B * D)
+            Bm, D, Tr, n = self.Bm, self.D, self.Tr, self.world * self.Bm
+            sub = idx if self.M == 1 else PackedIndices.columns(idx, m * n, (m + 1) * n)
+            self.ops.lookup_blocked(sub, self.send[m], D, Bm * D, Bm, Tr * Bm * D)
 
-    def seg_interact(self, x, dout):
-        self.ops.interact_fwd_recv(x, self.out, self.padding)
-        self.interact_bwd(dout, x)
+    def seg_interact(self, x, dout, m=0):
+        r = self.rows(m)
+        self.ops.interact_fwd_recv(x[r], self.out[r], self.padding, m)
+        self.interact_bwd(dout, x, m)
 
-    def interact_bwd(self, dout, x):
-        """dot_back, its table gradients in the exchange layout: one launch where the ops offer it
-        (the backward's stores go straight to gsend), else dt + the repack."""
+    def interact_bwd(self, dout, x, m=0):
+        """dot_back of micro-batch m, its table gradients in the exchange layout: one launch where the
+        ops offer it (the backward's stores go straight to gsend[m]), else dt + the repack."""
+        r = self.rows(m)
         send = getattr(self.ops, "interact_bwd_send", None)
         if send is not None and self._fused_bwd is not False:
-            self._fused_bwd = send(dout, x, self.dx, self.gsend, self.gs_base, self.gs_ld, self.padding)
+            self._fused_bwd = send(dout[r], x[r], self.dx[r], self.gsend[m], self.gs_base, self.gs_ld, self.padding, m)
             if self._fused_bwd:
                 return
         if self.dt is None:
-            self.dt = torch.empty((self.B, self.F * self.D), dtype=torch.float32, device=self.dx.device)
-        self.ops.interact_bwd_recv(dout, x, self.dx, self.dt, self.padding)
-        self.pack_grad()
+            self.dt = torch.empty((self.Bm, self.F * self.D), dtype=torch.float32, device=self.dx.device)
+        self.ops.interact_bwd_recv(dout[r], x[r], self.dx[r], self.dt, self.padding, m)
+        self.pack_grad(m)
 
     def seg_update(self, idx):
         if self.Tr:
@@ -290,69 +331,100 @@ class ShardedHotPath:
 
     def forward(self, x, idx):
         self.seg_index(idx)
-        self.seg_lookup(idx)
-        self.exchange_fwd()
-        self.ops.interact_fwd_recv(x, self.out, self.padding)
+        for m in range(self.M):
+            self.seg_lookup(idx, m)
+            self.exchange_fwd(m)
+            r = self.rows(m)
+            self.ops.interact_fwd_recv(x[r], self.out[r], self.padding, m)
         return self.out
 
     def backward(self, idx, dout, x):
-        self.interact_bwd(dout, x)
-        self.exchange_bwd()
+        for m in range(self.M):
+            self.interact_bwd(dout, x, m)
+            self.exchange_bwd(m)
         self.seg_update(idx)
         return self.dx
 
+    # ---- one step: compute on the current stream, exchanges on the comm stream
+    def _run(self, idx, lookup, interact, update, index):
+        """The step's schedule with the segments as callables (eager launches or graph replays)."""
+        M = self.M
+        if self._cstream is None:  # CPU (gloo tests): the same order, one stream
+            index()
+            for m in range(M):
+                lookup(m)
+                self.exchange_fwd(m)
+            for m in range(M):
+                interact(m)
+                self.exchange_bwd(m)
+            update()
+            return
+        main, cs = torch.cuda.current_stream(), self._cstream
+        ev_look, ev_recv, ev_bwd, _ = self._ev
+        self._side.wait_stream(main)  # the previous step's update read the indexer it rebuilds
+        with torch.cuda.stream(self._side):
+            index()
+            self._ix_done.record(self._side)
+        for m in range(M):
+            lookup(m)
+            ev_look[m].record(main)
+            cs.wait_event(ev_look[m])
+            with torch.cuda.stream(cs):
+                self.exchange_fwd(m)
+                ev_recv[m].record(cs)
+        for m in range(M):
+            main.wait_event(ev_recv[m])
+            interact(m)
+            ev_bwd[m].record(main)
+            cs.wait_event(ev_bwd[m])
+            with torch.cuda.stream(cs):
+                self.exchange_bwd(m)
+        main.wait_stream(cs)
+        main.wait_event(self._ix_done)
+        update()
+
     def step(self, x, idx, dout):
-        self.seg_index(idx)
-        self.seg_lookup(idx)
-        self.exchange_fwd()
-        self.seg_interact(x, dout)
-        self.exchange_bwd()
-        self.seg_update(idx)
+        self._run(idx, lambda m: self.seg_lookup(idx, m), lambda m: self.seg_interact(x, dout, m),
+                  lambda: self.seg_update(idx), lambda: self.seg_index(idx))
         return self.dx
 
     # ---- hipGraph replay of the compute segments (collectives stay eager)
     def capture(self, x, idx_list, dout):
-        """Captures seg_index (side stream) / seg_lookup / seg_update per index batch and
-        seg_interact once."""
-        s = torch.cuda.Stream(device=self.send.device)
+        """Captures seg_index / seg_lookup(m) / seg_update per index batch and seg_interact(m) once."""
+        s = torch.cuda.Stream(device=self.out.device)
         s.wait_stream(torch.cuda.current_stream())
         look, upd, ixg = [], [], []
+
+        def graph(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                fn()
+            return g
         with torch.cuda.stream(s):
             for idx in idx_list:
-                for lst, fn in ((ixg, self.seg_index), (look, self.seg_lookup), (upd, self.seg_update)):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
-                        fn(idx)
-                    lst.append(g)
-            mid = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(mid, stream=s):
-                self.seg_interact(x, dout)
+                ixg.append(graph(lambda: self.seg_index(idx)))
+                look.append([graph(lambda: self.seg_lookup(idx, m)) for m in range(self.M)])
+                upd.append(graph(lambda: self.seg_update(idx)))
+            mid = [graph(lambda: self.seg_interact(x, dout, m)) for m in range(self.M)]
         torch.cuda.current_stream().wait_stream(s)
         self._graphs = (look, mid, upd, ixg)
-        self._ix_done = torch.cuda.Event()
 
     def step_graphed(self, k):
-        """One step: the indexer build runs on a side stream beside the lookup, the exchanges
-        and the interaction; the update waits for it.  The side stream first waits for the
-        previous step's update (the indexer buffers are reused)."""
+        """One step of index batch k from the captured graphs (same schedule as `step`)."""
         look, mid, upd, ixg = self._graphs
-        main = torch.cuda.current_stream()
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            ixg[k].replay()
-            self._ix_done.record(self._side)
-        look[k].replay()
-        self.exchange_fwd()
-        mid.replay()
-        self.exchange_bwd()
-        main.wait_event(self._ix_done)
-        upd[k].replay()
+        self._run(None, lambda m: look[k][m].replay(), lambda m: mid[m].replay(), lambda: upd[k].replay(),
+                  lambda: ixg[k].replay())
 
 
-def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None, nbatch=8):
+def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None, nbatch=8,
+                      micro=None):
     """Bench setup for one rank: local tables (full size) and nbatch index batches for the
-    global batch; returns (engine, step(k) closure, prepare_graphs() closure)."""
+    global batch; returns (engine, step(k) closure, prepare_graphs() closure).  batch_local =
+    global batch / world for strong scaling.  micro: micro-batches per step (default: 2 where
+    the rank's batch splits into halves of >= 128 samples, else 1)."""
     import numpy as np
+    if micro is None:
+        micro = 2 if batch_local % 2 == 0 and batch_local >= 256 else 1
     rows = w["rows"]
     D, L = w["dim"], w["lookups"]
     E = 4 if w["dtype"] == "f32" else 2
@@ -369,7 +441,7 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
         tables.append(torch.empty((n, D), dtype=dt, device=device).uniform_(-s, s, generator=g))
     Bg = batch_local * world
     ops = HipShardOps(tables, Bg, L, lr, device=device)
-    eng = ShardedHotPath(ops, part, rank, batch_local, D, L, dt, device)
+    eng = ShardedHotPath(ops, part, rank, batch_local, D, L, dt, device, micro=micro)
     nb = nbatch
     packs = []
     zipf = w.get("zipf")

@@ -32,14 +32,17 @@ def host_rows(t, rows):
     return sel.cpu().numpy() if t.dtype == torch.float32 else bf16_bits(sel)
 
 
-def compact(tables, idx_np):
-    """(unique rows per table, compact host tables, renumbered indices [T][N] int64)."""
-    uniq, comp, ridx = [], [], np.empty_like(idx_np, dtype=np.int64)
+def compact(tables, idx_list):
+    """(unique rows per table, compact host tables, per batch the renumbered indices [T][N] int64):
+    the rows every batch of idx_list touches, renumbered consistently across the batches."""
+    uniq, comp = [], []
+    ridx = [np.empty_like(i, dtype=np.int64) for i in idx_list]
     for t, tab in enumerate(tables):
-        u, inv = np.unique(idx_np[t], return_inverse=True)
+        u = np.unique(np.concatenate([i[t] for i in idx_list]))
         uniq.append(u)
         comp.append(host_rows(tab, u))
-        ridx[t] = inv
+        for k, i in enumerate(idx_list):
+            ridx[k][t] = np.searchsorted(u, i[t])
     return uniq, comp, ridx
 
 
@@ -47,49 +50,74 @@ def to_f32(a):
     return oracle.bf16_to_f32(a) if a.dtype == np.uint16 else a
 
 
-def zipf_indices(pkg, rng, rows, n, s):
-    return np.stack([pkg.zipf_rows(rng, r, n, s, pkg.zipf_perm(rng, r)) for r in rows]).astype(np.int64)
+def zipf_indices(pkg, rng, rows, n, s, perms=None):
+    perms = perms or [pkg.zipf_perm(rng, r) for r in rows]
+    return np.stack([pkg.zipf_rows(rng, r, n, s, p) for r, p in zip(rows, perms)]).astype(np.int64)
 
 
-def run_step_vs_oracle(pkg, gpu, tables, idx_np, B, L, lr, dtype, seed, hot_kw=None):
-    """One HotPath training step on the device tables against the oracle's step on their touched
-    rows.  Returns nothing; asserts out, dx, touched rows after the update, untouched rows."""
+def run_step_vs_oracle(pkg, gpu, tables, idx_np, B, L, lr, dtype, seed, hot_kw=None, pipeline=None):
+    """Training steps on the device tables, in the form bench.py times (`pipeline`, from
+    pkg.step_pipeline: None = indexer in the forward's launch, "side" = the next batch's indexer on
+    a side stream, "apply" = built by the previous step's apply launch), against the oracle's
+    steps on the rows they touch.  idx_np: one [T][B*L] batch, or a list of two consecutive batches
+    (a pipelined step then consumes the indexer the previous step prepared).  Asserts the last
+    step's out and dx, every touched row after all steps, and that untouched rows are unchanged."""
     T, D = len(tables), tables[0].shape[1]
     F = T + 1
-    uniq, comp, ridx = compact(tables, idx_np)
+    batches = idx_np if isinstance(idx_np, list) else [idx_np]
+    uniq, comp, ridx = compact(tables, batches)
     before = [t.clone() for t in tables] if sum(t.numel() for t in tables) * 2 < 40e9 else None
     rng = np.random.default_rng(seed)
     x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(dtype).to(gpu)
     ts = pkg.EmbeddingTableSet(tables)
-    hp = pkg.HotPath(ts, B, L, lr=lr, index_base=0, **(hot_kw or {}))
+    hp = pkg.HotPath(ts, B, L, lr=lr, index_base=0, pipeline=pipeline, **(hot_kw or {}))
+    assert hp.pipeline == pipeline, (hp.pipeline, pipeline)
     dout = torch.from_numpy((rng.standard_normal((B, hp.width)) * 1e-2).astype(np.float32)).to(dtype).to(gpu)
-    p = pkg.PackedIndices(torch.from_numpy(idx_np).to(torch.int32).to(gpu).reshape(T, B, L))
-    hp.validate(x, p, dout)
-    hp.step(x, p, dout)
+    P = [pkg.PackedIndices(torch.from_numpy(i).to(torch.int32).to(gpu).reshape(T, B, L)) for i in batches]
+    for p in P:
+        hp.validate(x, p, dout)
+    n = len(P)
+    if pipeline == "apply":  # prime = one step of the last batch, preparing batch 0
+        hp.prime(P[0], x=x, dout=dout, prev=P[-1])
+        for k in range(n):
+            hp.step_prep(x, P[k], dout, P[(k + 1) % n])
+        order = [n - 1] + list(range(n))
+    elif pipeline == "side":
+        hp.prime(P[0])
+        for k in range(n):
+            hp.step_next(x, P[k], dout, P[(k + 1) % n])
+        order = list(range(n))
+    else:
+        for k in range(n):
+            hp.step(x, P[k], dout)
+        order = list(range(n))
     torch.cuda.synchronize()
     hp.check_bounds()
-    # the oracle's step on the compact tables
+    # the oracle's steps on the compact tables
     xh = x.cpu().numpy() if dtype == torch.float32 else bf16_bits(x)
     dh = dout.cpu().numpy() if dtype == torch.float32 else bf16_bits(dout)
-    ys = np.zeros((B, F * D), dtype=xh.dtype)
-    oracle.maplookup(comp, ridx, 0, B, L, ys, D)
-    out = oracle.interact_fwd(xh, ys, F, hp.padding)
-    dx, dt = oracle.interact_bwd(dh, ys, D, F, hp.padding)
-    oracle.sgd_update(comp, ridx, 0, B, L, dt, D, lr)
+    for k in order:
+        ys = np.zeros((B, F * D), dtype=xh.dtype)
+        oracle.maplookup(comp, ridx[k], 0, B, L, ys, D)
+        out = oracle.interact_fwd(xh, ys, F, hp.padding)
+        dx, dt = oracle.interact_bwd(dh, ys, D, F, hp.padding)
+        oracle.sgd_update(comp, ridx[k], 0, B, L, dt, D, lr)
     bf = dtype == torch.bfloat16
     got_out = hp.out.float().cpu().numpy()
-    if bf:  # one bf16 rounding of an fp32 sum that may differ in order: 2 ulp of bf16
+    nsteps = len(order)
+    if bf:  # one bf16 rounding of an fp32 sum that may differ in order (2 ulp of bf16), on rows that
+        # earlier steps rounded to bf16 on each side (1 ulp per step apart)
         err = np.abs(got_out - to_f32(out))
-        assert (err <= 2.0 ** -7 * np.abs(to_f32(out)) + 1e-6).all(), ("out", err.max())
+        assert (err <= 2.0 ** -7 * nsteps * np.abs(to_f32(out)) + 1e-6).all(), ("out", err.max())
     else:
         assert_close(got_out, out, rtol=1e-5, scale=np.abs(out).max(), what="out")
-    assert_close(hp.dx.cpu().numpy(), dx, rtol=1e-4 if bf else 1e-5, scale=np.abs(dx).max(), what="dx")
+    assert_close(hp.dx.cpu().numpy(), dx, rtol=1e-4 * nsteps if bf else 1e-5, scale=np.abs(dx).max(), what="dx")
     for t, tab in enumerate(tables):
         got = to_f32(host_rows(tab, uniq[t]))
         want = to_f32(comp[t])
-        if bf:  # the same fp32 update, each side rounded once to bf16: at most 1 ulp (2^-7 relative) apart
+        if bf:  # the same fp32 update, each side rounded once to bf16 per step: 1 ulp (2^-7 relative) per step
             err = np.abs(got - want)
-            assert (err <= 2.0 ** -7 * np.abs(want) + 1e-30).all(), (t, err.max())
+            assert (err <= 2.0 ** -7 * nsteps * np.abs(want) + 1e-30).all(), (t, err.max())
         else:
             g = np.abs(to_f32(host_rows(before[t], uniq[t])) - want) if before is not None else np.abs(want)
             assert_close(got, want, rtol=1e-5, scale=g.max() + 1e-6, what=f"table {t} rows")
@@ -98,6 +126,30 @@ def run_step_vs_oracle(pkg, gpu, tables, idx_np, B, L, lr, dtype, seed, hot_kw=N
             mask[torch.from_numpy(uniq[t]).to(gpu)] = False
             assert torch.equal(tab[mask], before[t][mask]), f"table {t}: an untouched row changed"
     return hp
+
+
+# ------------------------------------------------------- the bench's exact forms, full size
+def kaggle_tables(pkg, gpu, D, dtype, seed):
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    return [torch.empty((n, D), dtype=dtype, device=gpu).uniform_(-n ** -0.5, n ** -0.5, generator=g)
+            for n in pkg.KAGGLE_EMBEDDING_SIZES]
+
+
+@pytest.mark.parametrize("workload", ["kaggle-d128-b2048", "kaggle-d16-b2048", "kaggle-d128-b8192-bf16"])
+def test_bench_form_vs_oracle(pkg, gpu, workload):
+    """The exact step form bench.py times for each Kaggle-row workload (pkg.step_pipeline: the
+    metric config builds its indexer in the forward's launch, D = 16 in the previous step's apply
+    launch, bf16 B = 8192 on a side stream), over two consecutive batches so the prepared indexer is
+    consumed, at full table size, against the oracle on the touched rows (validation.jl:125-146)."""
+    w = pkg.WORKLOADS[workload]
+    D, B = w["dim"], w["batch"]
+    dtype = torch.float32 if w["dtype"] == "f32" else torch.bfloat16
+    tables = kaggle_tables(pkg, gpu, D, dtype, seed=D + B)
+    rng = np.random.default_rng(B + D)
+    batches = [np.stack([rng.integers(0, n, size=B) for n in w["rows"]]).astype(np.int64) for _ in range(2)]
+    pipeline = pkg.step_pipeline(w)
+    hp = run_step_vs_oracle(pkg, gpu, tables, batches, B, 1, 0.05, dtype, seed=B, pipeline=pipeline)
+    assert hp.step_api
 
 
 # ---------------------------------------------------------------------------- configs[2]
@@ -172,7 +224,7 @@ def test_terabyte_bf16_full_size(pkg, gpu):
     """configs[3] on one GPU: the 26 Criteo-Terabyte tables (882.8M rows x 128 bf16 = 226 GB,
     criteo.jl:379-406).  (1) Row-encoded gather: columns 0-3 of row r hold its four bytes and
     column 4 the table, so every gathered row identifies itself exactly (bf16 holds 0-255).
-    (2) A Zipf(1.05) training step (the bench's workload) against the oracle on its touched rows.
+    (2) The bench's pipelined step form over two Zipf(1.05) batches against the oracle on their touched rows.
     (3) An integer-gradient update on zeroed tables == the closed form, bit for bit."""
     rows = pkg.TERABYTE_EMBEDDING_SIZES
     T, D, B = len(rows), 128, 2048
@@ -188,7 +240,9 @@ def test_terabyte_bf16_full_size(pkg, gpu):
                 tab[r0:r0 + len(r), k] = ((r >> (8 * k)) & 255).to(torch.bfloat16)
             tab[r0:r0 + len(r), 4] = float(t)
     rng = np.random.default_rng(41)
-    idx_np = zipf_indices(pkg, rng, rows, B, 1.05)
+    perms = [pkg.zipf_perm(rng, r) for r in rows]  # the same rows stay hot across batches
+    idx_np = zipf_indices(pkg, rng, rows, B, 1.05, perms)
+    idx2_np = zipf_indices(pkg, rng, rows, B, 1.05, perms)
     idx = torch.from_numpy(idx_np).to(torch.int32).to(gpu)
     ts = pkg.EmbeddingTableSet(tables)
     ys = pkg.maplookup(pkg.PreallocationStrategy(D), ts, pkg.PackedIndices(idx), index_base=0)
@@ -197,12 +251,18 @@ def test_terabyte_bf16_full_size(pkg, gpu):
     assert torch.equal(dec, idx.T.to(torch.int64))
     assert torch.equal(got[:, :, 4], torch.arange(T, device=gpu, dtype=torch.float32)[None, :].expand(B, T))
     del ys, got
-    # (2) the training step vs the oracle (fresh random rows where the step reads and writes)
+    # (2) the bench's step form (pkg.step_pipeline: the indexer built by the previous step's apply
+    # launch, 8 parts per table) over two consecutive batches vs the oracle (fresh random rows where
+    # the steps read and write)
     g = torch.Generator(device=gpu).manual_seed(42)
+    idx2 = torch.from_numpy(idx2_np).to(torch.int32).to(gpu)
     for t, tab in enumerate(tables):
-        u = torch.unique(idx[t].long())
+        u = torch.unique(torch.cat([idx[t], idx2[t]]).long())
         tab[u] = torch.empty((len(u), D), device=gpu).uniform_(-0.05, 0.05, generator=g).to(torch.bfloat16)
-    hp = run_step_vs_oracle(pkg, gpu, tables, idx_np, B, 1, 0.05, torch.bfloat16, seed=43)
+    pipeline = pkg.step_pipeline(pkg.WORKLOADS["terabyte-d128-bf16-zipf"])
+    assert pipeline == "apply"
+    hp = run_step_vs_oracle(pkg, gpu, tables, [idx_np, idx2_np], B, 1, 0.05, torch.bfloat16, seed=43,
+                            pipeline=pipeline)
     del hp
     # (3) exact integer-gradient update on zeroed tables
     for tab in tables:

@@ -799,7 +799,7 @@ def _shard_owners(case, owners, world):
     return part.owners
 
 
-def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, case="small"):
+def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, case="small", micro=1):
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -816,9 +816,9 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, cas
     part = TablePartition(T, world, _shard_owners(case, owners, world))
     mine = part.tables(rank)
     ops = HipShardOps([torch.from_numpy(tabs[t]).to(dev) for t in mine], Bg, L, 0.25, device=dev)
-    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, dev)
+    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, dev, micro=micro)
     p = pkg.PackedIndices(torch.from_numpy(idx[mine]).to(torch.int32).reshape(len(mine), Bg, L).to(dev))
-    sl = slice(rank * B, (rank + 1) * B)
+    sl = [eng.global_index(b) for b in range(B)]  # this rank's samples of the global batch
     xd, dd = torch.from_numpy(x[sl]).to(dev), torch.from_numpy(dout[sl]).to(dev)
     if graphed:  # the bench's form: compute segments replayed as hipGraphs around eager exchanges
         eng.capture(xd, [p], dd)
@@ -833,10 +833,13 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, cas
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("owners,graphed,case", [(None, False, "small"), ([[4, 0, 2], [1, 3]], True, "small"),
-                                                 ("fitting", True, "terabyte-scaled"),
-                                                 (None, True, "kaggle-scaled-d128")])
-def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed, case):
+@pytest.mark.parametrize("owners,graphed,case,micro", [
+    (None, False, "small", 1), ([[4, 0, 2], [1, 3]], True, "small", 1), ("fitting", True, "terabyte-scaled", 1),
+    (None, True, "kaggle-scaled-d128", 1),
+    # micro-batches: exchange of one half overlapping the compute of the other (comm stream)
+    (None, False, "small", 2), ([[4, 0, 2], [1, 3]], True, "small", 4), ("fitting", True, "terabyte-scaled", 2),
+    (None, True, "kaggle-scaled-d128", 2)])
+def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, graphed, case, micro):
     """The table-sharded step (HIP kernels, 2 ranks sharing the GPU, gloo exchange; contiguous,
     explicit or TablePartition.fitting's byte-balanced non-contiguous assignment; eager or
     hipGraph-segment launches) equals the single-GPU HotPath on the global batch bit for bit.
@@ -849,8 +852,8 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, gra
     port = s.getsockname()[1]
     s.close()
     world = 2
-    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path), owners, graphed, case), nprocs=world,
-                       start_method="spawn")
+    mp.start_processes(_gpu_shard_worker, args=(world, port, str(tmp_path), owners, graphed, case, micro),
+                       nprocs=world, start_method="spawn")
     rows, D, B, L, tabs, idx, x, dout = _shard_inputs(case, world)
     T, Bg = len(rows), B * world
     hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), Bg, L, lr=0.25, index_base=0)
@@ -858,9 +861,10 @@ def test_sharded_two_ranks_equal_single_gpu_step(pkg, gpu, tmp_path, owners, gra
     hp.step(torch.from_numpy(x).to(gpu), p, torch.from_numpy(dout).to(gpu))
     from dlrm_jl_amd.sharded import TablePartition
     part = TablePartition(T, world, _shard_owners(case, owners, world))
+    Bm = B // micro
     for r in range(world):
         z = np.load(tmp_path / f"g{r}.npz")
-        sl = slice(r * B, (r + 1) * B)
+        sl = [(b // Bm) * world * Bm + r * Bm + b % Bm for b in range(B)]
         assert np.array_equal(z["out"], to_np_f32(hp.out)[sl])
         assert np.array_equal(z["dx"], to_np_f32(hp.dx)[sl])
         for t in part.tables(r):

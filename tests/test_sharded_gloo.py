@@ -34,8 +34,8 @@ class OracleShardOps:
         self.tables = tables
         self.lr = lr
 
-    def bind_recv(self, tabs):
-        self.recv_tables = tabs
+    def bind_recv(self, tabs_per_mb):
+        self.recv_tables = tabs_per_mb
 
     def build_indexer(self, idx):
         pass
@@ -58,17 +58,18 @@ class OracleShardOps:
         d_ = (dbase.numpy()[None, :, None] + b * dld.numpy()[None, :, None] + c).reshape(-1)
         dst.view(-1).numpy()[d_] = src.reshape(-1).numpy()[s_]
 
-    def _ys(self, x):
-        return torch.cat([x] + list(self.recv_tables), dim=1).numpy()
+    def _ys(self, x, m):
+        return torch.cat([x] + list(self.recv_tables[m]), dim=1).numpy()
 
-    def interact_fwd_recv(self, x, out, padding):
-        ys = self._ys(x)
-        res = self.o.interact_fwd(x.numpy(), ys, len(self.recv_tables) + 1, padding)
+    def interact_fwd_recv(self, x, out, padding, m=0):
+        ys = self._ys(x, m)
+        res = self.o.interact_fwd(x.contiguous().numpy(), ys, len(self.recv_tables[m]) + 1, padding)
         out.copy_(torch.from_numpy(res))
 
-    def interact_bwd_recv(self, dout, x, dx, dt, padding):
+    def interact_bwd_recv(self, dout, x, dx, dt, padding, m=0):
         d = dx.shape[1]
-        rdx, rdt = self.o.interact_bwd(dout.numpy(), self._ys(x), d, len(self.recv_tables) + 1, padding)
+        rdx, rdt = self.o.interact_bwd(dout.contiguous().numpy(), self._ys(x, m), d, len(self.recv_tables[m]) + 1,
+                                       padding)
         dx.copy_(torch.from_numpy(rdx))
         dt.copy_(torch.from_numpy(rdt))
 
@@ -94,14 +95,14 @@ def _worker(rank, world, port, cfg, outdir):
     import dlrm_pkg
     pkg = dlrm_pkg.load()
     from dlrm_jl_amd.sharded import ShardedHotPath, TablePartition
-    T, rows, D, B, L, lr, owners = cfg
+    T, rows, D, B, L, lr, owners, micro = cfg
     tables, idx, x, dout = _problem(T, rows, D, B, world, L)
     part = TablePartition(T, world, owners)
     mine = part.tables(rank)
     ops = OracleShardOps([tables[t].copy() for t in mine], lr)
-    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, torch.device("cpu"))
+    eng = ShardedHotPath(ops, part, rank, B, D, L, torch.float32, torch.device("cpu"), micro=micro)
     p = pkg.PackedIndices(torch.from_numpy(idx[mine]).reshape(len(mine), B * world, L))
-    sl = slice(rank * B, (rank + 1) * B)
+    sl = [eng.global_index(b) for b in range(B)]  # this rank's samples of the global batch
     eng.step(torch.from_numpy(x[sl]).contiguous(), p, torch.from_numpy(dout[sl]).contiguous())
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), out=eng.out.numpy(), dx=eng.dx.numpy(),
              **{f"table{t}": ops.tables[k] for k, t in enumerate(mine)})
@@ -109,14 +110,17 @@ def _worker(rank, world, port, cfg, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,T,L,owners", [(2, 5, 1, None), (2, 7, 3, None), (3, 4, 1, None), (3, 2, 2, None),
-                                               (2, 5, 1, [[4, 0, 2], [1, 3]]), (3, 6, 2, [[5], [0, 2, 3, 4], [1]])])
-def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners):
-    """owners: explicit (non-contiguous) table assignment, as TablePartition.fitting makes."""
+@pytest.mark.parametrize("world,T,L,owners,micro", [
+    (2, 5, 1, None, 1), (2, 7, 3, None, 1), (3, 4, 1, None, 1), (3, 2, 2, None, 1),
+    (2, 5, 1, [[4, 0, 2], [1, 3]], 1), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 1),
+    (2, 5, 1, None, 2), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 2), (2, 7, 1, None, 4)])
+def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners, micro):
+    """owners: explicit (non-contiguous) table assignment, as TablePartition.fitting makes.
+    micro: micro-batches per step (rank r's local sample b is global sample global_index(r, b))."""
     import oracle
     rows = [3, 50, 1000, 7, 400, 12, 90][:T]
     D, B, lr = 16, 4, 0.5
-    cfg = (T, rows, D, B, L, lr, owners)
+    cfg = (T, rows, D, B, L, lr, owners, micro)
     mp.start_processes(_worker, args=(world, _free_port(), cfg, str(tmp_path)), nprocs=world, start_method="spawn")
     # single process on the global batch
     tables, idx, x, dout = _problem(T, rows, D, B, world, L)
@@ -129,9 +133,10 @@ def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners):
     oracle.sgd_update(tables, idx, 0, Bg, L, dt, D, lr)
     from dlrm_jl_amd.sharded import TablePartition
     part = TablePartition(T, world, owners)
+    Bm = B // micro
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")
-        sl = slice(r * B, (r + 1) * B)
+        sl = [(b // Bm) * world * Bm + r * Bm + b % Bm for b in range(B)]
         assert np.array_equal(z["out"], out[sl])
         assert np.array_equal(z["dx"], dx[sl])
         for t in part.tables(r):

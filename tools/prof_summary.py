@@ -8,6 +8,9 @@
   gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the bytes of a wide
   coalesced read stream, so HBM read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
   16-B stores.  hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+* MFMA pass (--pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, own run): mfma_busy = the MFMA busy
+  cycles summed over the chip / (1024 SIMDs x GRBM_GUI_ACTIVE cycles of the dispatch), i.e. the
+  fraction of SIMD-cycles the matrix cores were busy (north_star's MFMA utilisation).
 Writes <out>.json (consumed by bench.py for roofline.traffic) and <out>.md.
 """
 import argparse
@@ -19,8 +22,8 @@ import re
 from collections import defaultdict
 
 STAGES = [  # (regex on the kernel name, stage)
-    (r"interact_fwd_kernel<[^,]+, \d+, true(, \d+)?>|interact_fwd_index_kernel", "lookup_interact_fwd"),
-    (r"interact_fwd_kernel<[^,]+, \d+, false(, \d+)?>|interact_fwd_scalar", "interact_fwd"),
+    (r"interact_fwd_kernel<[^,]+, \d+, true|interact_fwd_index_kernel", "lookup_interact_fwd"),
+    (r"interact_fwd_kernel<[^,]+, \d+, false|interact_fwd_scalar", "interact_fwd"),
     (r"interact_bwd", "interact_bwd"),  # incl. interact_bwd_index_kernel
     (r"maplookup_", "lookup"),
     (r"indexer_build_kernel|indexer_fast_kernel|hix_", "indexer_build"),
@@ -68,6 +71,8 @@ def main():
     ap.add_argument("--kt", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--mfma")
+    ap.add_argument("--head", default="unknown", help="git HEAD the profiled library was built from")
     ap.add_argument("--workload", default="kaggle-d128-b2048")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -78,6 +83,8 @@ def main():
         kernels[short(r["Name"])] = {"stage": stage_of(r["Name"]), "calls": int(r["Calls"]),
                                      "avg_us": float(r["AverageNs"]) / 1e3, "min_us": float(r["MinNs"]) / 1e3,
                                      "max_us": float(r["MaxNs"]) / 1e3}
+    mfma = counters(a.mfma, "SQ_VALU_MFMA_BUSY_CYCLES") if a.mfma else {}
+    gui = counters(a.mfma, "GRBM_GUI_ACTIVE") if a.mfma else {}
     fetch = counters(a.fetch, "FETCH_SIZE") if a.fetch else {}
     write = counters(a.write, "WRITE_SIZE") if a.write else {}
     for k, v in kernels.items():
@@ -89,6 +96,11 @@ def main():
             v["WRITE_SIZE_KB_avg"] = sum(w) / len(w)
         if f and w:
             v["hbm_bytes_per_launch"] = int(2 * v["FETCH_SIZE_KB_avg"] * 1024 + v["WRITE_SIZE_KB_avg"] * 1024)
+        m, g = mfma.get(k), gui.get(k)
+        if m and g:
+            v["MFMA_BUSY_CYCLES_avg"] = sum(m) / len(m)
+            v["GRBM_GUI_ACTIVE_avg"] = sum(g) / len(g)
+            v["mfma_busy"] = v["MFMA_BUSY_CYCLES_avg"] / (1024.0 * v["GRBM_GUI_ACTIVE_avg"])
     stages = defaultdict(lambda: {"avg_us": 0.0, "kernels": []})
     for k, v in kernels.items():
         if v["stage"] is None:
@@ -98,17 +110,19 @@ def main():
         s["kernels"].append(k)
         if "hbm_bytes_per_launch" in v:
             s["hbm_bytes_per_launch"] = s.get("hbm_bytes_per_launch", 0) + v["hbm_bytes_per_launch"]
-    out = {"workload": a.workload, "kernels": kernels, **{k: dict(v) for k, v in stages.items()}}
+        if "mfma_busy" in v:
+            s["mfma_busy"] = max(s.get("mfma_busy", 0.0), v["mfma_busy"])
+    out = {"workload": a.workload, "head": a.head, "kernels": kernels, **{k: dict(v) for k, v in stages.items()}}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out + ".json", "w") as f:
         json.dump(out, f, indent=1)
-    lines = [f"# rocprofv3 summary — {a.workload}", "",
-             "| kernel | stage | calls | avg µs | min µs | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2·F+W) |",
-             "|---|---|---|---|---|---|---|---|"]
+    lines = [f"# rocprofv3 summary — {a.workload} (library built at {a.head})", "",
+             "| kernel | stage | calls | avg µs | min µs | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2·F+W) | MFMA busy |",
+             "|---|---|---|---|---|---|---|---|---|"]
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_us"]):
         lines.append(f"| `{k}` | {v['stage']} | {v['calls']} | {v['avg_us']:.2f} | {v['min_us']:.2f} | "
                      f"{v.get('FETCH_SIZE_KB_avg', float('nan')):.0f} | {v.get('WRITE_SIZE_KB_avg', float('nan')):.0f} | "
-                     f"{v.get('hbm_bytes_per_launch', '—')} |")
+                     f"{v.get('hbm_bytes_per_launch', '—')} | {v.get('mfma_busy', float('nan')):.3f} |")
     with open(a.out + ".md", "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
