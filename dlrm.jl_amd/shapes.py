@@ -41,7 +41,7 @@ WORKLOADS = {
 
 def step_pipeline(w):
     """Where the training step's split indexer is built for workload `w` (the form bench.py times
-    and tests/test_configs.py checks against the oracle): "apply" = inside the previous step's apply
+    and tests/test_configs.py checks step by step on the CPU checker): "apply" = inside the previous step's apply
     launch (rows of <= 256 B, batches <= 2048: the forward then only gathers), "side" = the next
     batch's build on a side stream (one-hot batches > 2048), None = inside the forward's launch."""
     E = 4 if w["dtype"] == "f32" else 2
