@@ -57,6 +57,8 @@ def parse():
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
                          "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
     ap.add_argument("--stage-timing", type=int, default=1, help="0: skip the per-stage telemetry (traces)")
+    ap.add_argument("--chain", type=int, default=1,
+                    help="1: also time the reference's operator chain on HipTables (the drop-in path; one GPU)")
     ap.add_argument("--nbatch", type=int, default=NBATCH, help="distinct index batches cycled")
     ap.add_argument("--sustain", type=float, default=2.0,
                     help="seconds of back-to-back steps timed after the K-step region (reported as 'sustained')")
@@ -401,6 +403,53 @@ def main():
                      "value": round(B * world / (ms_s / 1e3), 1)}
     value = B * world / (ms / 1e3)
 
+    # ---- the drop-in operator chain (what an unchanged train! drives through the shim:
+    # maplookup -> rrule(DotInteraction) -> pullback -> maplookup_pullback -> update!) on HipTables,
+    # i.e. the fused step kernels reached through the reference's operator API (dlrm.jl_amd/lazy.py)
+    chain = None
+    if world == 1 and L == 1 and a.chain and graphs is not None:
+        ht = pkg.HipTables(ts, lr=a.lr)
+        dot = pkg.DotInteraction()
+        strat = pkg.PreallocationStrategy(D)
+
+        def chain_step(k):
+            p = packs[k % nb]
+            ys = pkg.maplookup(strat, ht, p)
+            _, back = pkg.rrule(dot, x, ys)
+            _, _, dy = back(dout)
+            pkg.update_(pkg.Descent(a.lr), ht, pkg.maplookup_pullback(D, ht, p, dy), check_bounds=False)
+
+        try:
+            for k in range(2):
+                chain_step(k)
+            gs = {}
+            for piece in set(plan(a.steps)) | set(plan(a.warmup)):
+                cur = torch.cuda.current_stream()
+                s_ = torch.cuda.Stream()
+                s_.wait_stream(cur)
+                with torch.cuda.stream(s_):
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=s_):
+                        for k in range(piece[0], piece[0] + piece[1]):
+                            chain_step(k)
+                cur.wait_stream(s_)
+                gs[piece] = gr
+            for piece in plan(a.warmup):
+                gs[piece].replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for piece in plan(a.steps):
+                gs[piece].replay()
+            torch.cuda.synchronize()
+            ms_c = (time.perf_counter() - t0) * 1e3 / a.steps
+            ht.hotpath(B).check_bounds()
+            chain = {"value": round(B / (ms_c / 1e3), 1), "ms_per_step": round(ms_c, 4),
+                     "vs_step": round(ms / ms_c, 3),
+                     "form": "maplookup(HipTables) -> rrule(DotInteraction) -> pullback -> maplookup_pullback -> "
+                             "update!(Descent): dlrm_step_fwd / dlrm_step_bwd(BWD_ONLY) / (APPLY_ONLY), hipGraph replay"}
+        except Exception as e:
+            print(f"note: drop-in chain timing failed ({e!r})", file=sys.stderr)
+
     # ---- per-kernel timing (HIP events on the launch stream) + roofline, rank 0
     roofline = None
     stages = None
@@ -588,7 +637,7 @@ def main():
                                 if world == 1 and engine.pipeline else
                                 "dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "
                                 "updated in the backward)" if world == 1 and engine.step_api else "operators")},
-            "sustained": sustained, "roofline": roofline, "cpu_baseline": cpu,
+            "sustained": sustained, "drop_in_chain": chain, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     if world > 1:

@@ -13,6 +13,7 @@ from .dense import DenseMLP, DLRMModel, ShardedDLRMModel, bce_loss, bce_loss_bac
 from .embedding import (DefaultStrategy, EmbeddingTableSet, PackedIndices, PreallocationStrategy, SimpleEmbedding,
                         lookup, maplookup)
 from .hotpath import HotPath
+from .lazy import DeferredUpdate, HipTables, LazyGrad, LazyLookup
 from .interact import (POST_INTERACTION_PAD_TO_MUL, DotInteraction, cdiv, dot_back, dot_interaction, fast_vcat,
                        interaction_sizes, rrule, rrule_dot_interaction, rrule_self_batched_mul, rrule_triangular_slice,
                        self_batched_mul, triangular_slice, triangular_slice_back, up_to_mul_of)
@@ -27,5 +28,6 @@ __all__ = [
     "SparseIndexer", "maplookup_pullback", "update_", "DenseMLP", "DLRMModel", "bce_loss", "bce_loss_back",
     "kaggle_mlp_sizes", "random_mlp", "dac", "DAC_DTYPE", "DACLoader", "DACMaps", "ShardedDLRMModel",
     "dot_interaction", "rrule_dot_interaction", "triangular_slice", "triangular_slice_back", "rrule_triangular_slice",
-    "self_batched_mul", "rrule_self_batched_mul", "step_pipeline", "zipf_perm",
+    "self_batched_mul", "rrule_self_batched_mul", "step_pipeline", "zipf_perm", "HipTables", "LazyLookup",
+    "LazyGrad", "DeferredUpdate",
 ]

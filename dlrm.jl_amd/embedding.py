@@ -186,7 +186,11 @@ def maplookup(strategy, tables, sparse, *, index_base=1, out=None, check_bounds=
     PreallocationStrategy(P): returns [B][P + D*T]; row b holds [<untouched P> | e_1 | ... | e_T]
     where e_t = sum_k table_t[idx_t[b, k]] (sum pooling for multi-hot bags).
     DefaultStrategy(): returns a list of per-table [B][D] tensors.
-    Raises BoundsError on an out-of-range index when check_bounds (synchronises)."""
+    Raises BoundsError on an out-of-range index when check_bounds (synchronises).
+    With `HipTables` (lazy.py): a LazyLookup, gathered by the interaction's fused kernel."""
+    from .lazy import HipTables, maplookup_lazy
+    if isinstance(tables, HipTables):
+        return maplookup_lazy(strategy, tables, sparse)
     ts = as_table_set(tables)
     idx = PackedIndices(sparse, device=ts.device)
     require_device(idx.data, ts.device, "indices")

@@ -40,6 +40,12 @@ class DotInteraction:
         self.pad_to = pad_to
 
     def __call__(self, x, ys, *, return_t=False, out=None):
+        from .lazy import LazyLookup
+        if isinstance(ys, LazyLookup):  # HipTables: the fused gather + interaction (dlrm_step_fwd)
+            if return_t or out is not None or self.pad_to != POST_INTERACTION_PAD_TO_MUL:
+                ys = ys.materialize()
+            else:
+                return ys.interact(x).out
         if x.dim() != 2 or ys.dim() != 2 or x.shape[0] != ys.shape[0]:
             raise ValueError("DotInteraction: x [B][d] and ys [B][d + D*T] expected")
         if x.dtype != ys.dtype:
@@ -90,7 +96,13 @@ def dot_back(dot, delta, t, xlen, padding, *, dx=None, dt=None):
 
 
 def rrule(dot, x, ys):
-    """ChainRulesCore.rrule(dot::DotInteraction, X, Y) (interact.jl:438-447)."""
+    """ChainRulesCore.rrule(dot::DotInteraction, X, Y) (interact.jl:438-447).  With a LazyLookup
+    (HipTables): the training step's forward, and a pullback running its backward (lazy.py)."""
+    from .lazy import LazyLookup, rrule_lazy
+    if isinstance(ys, LazyLookup) and dot.pad_to == POST_INTERACTION_PAD_TO_MUL:
+        return rrule_lazy(x, ys)
+    if isinstance(ys, LazyLookup):
+        ys = ys.materialize()
     forward, t, padding = dot(x, ys, return_t=True)
     xlen = x.shape[1]
 

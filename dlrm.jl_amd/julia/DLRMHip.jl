@@ -42,11 +42,16 @@ end
 
 mutable struct Context
     ptr::Ptr{Cvoid}
-    function Context(device::Integer; stream::Ptr{Cvoid} = C_NULL)
+    # fused = true: maplookup on this context's HipEmbeddings returns a HipLookup and the operator
+    # chain runs on the training-step kernels (see "The unchanged operator chain" below); lr: the
+    # Descent η of the update! that follows (lets the pullback step the once-hit rows itself)
+    fused::Bool
+    lr::Union{Nothing,Float32}
+    function Context(device::Integer; stream::Ptr{Cvoid} = C_NULL, fused::Bool = false, lr = nothing)
         out = Ref{Ptr{Cvoid}}(C_NULL)
         rc = ccall((:dlrm_ctx_create, libdlrm), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, stream, out)
         rc == 0 || throw(DLRMError(rc, "dlrm_ctx_create"))
-        ctx = new(out[])
+        ctx = new(out[], fused, lr === nothing ? nothing : Float32(lr))
         finalizer(c -> ccall((:dlrm_ctx_destroy, libdlrm), Cint, (Ptr{Cvoid},), c.ptr), ctx)
         return ctx
     end
@@ -183,7 +188,8 @@ function _maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse,
 end
 
 EmbeddingTables.maplookup(s::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding}, sparse) =
-    first(_maplookup(tables, sparse, prealloc_rows(s)))
+    first(tables).data.ctx.fused ? _fused_maplookup(tables, sparse, prealloc_rows(s)) :
+                                   first(_maplookup(tables, sparse, prealloc_rows(s)))
 
 # DefaultStrategy: one D x B matrix per table (test/model/embedding_update.jl:31, model.jl:155)
 function EmbeddingTables.maplookup(::DefaultStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}}, sparse) where {D}
@@ -215,9 +221,8 @@ const HipUpdate{D} = SparseEmbeddingUpdate{Static{D},HipDelta,HipIndices}
 hip_delta(u::SparseEmbeddingUpdate) = u.delta::HipDelta        # EmbeddingTables' field names
 hip_indices(u::SparseEmbeddingUpdate) = u.indices::HipIndices
 
-function ChainRulesCore.rrule(
-    ::typeof(maplookup), strategy::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}}, sparse
-) where {D}
+function _rrule_maplookup(strategy::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}},
+                          sparse) where {D}
     P = prealloc_rows(strategy)
     ys, idx = _maplookup(tables, sparse, P)
     function maplookup_pullback(dt)
@@ -345,6 +350,10 @@ function EmbeddingTables.update!(
             throw(ArgumentError("update! expects the per-table views of one maplookup pullback"))
     end
     ctx, idx = δ1.dt.ctx, ix1.idx
+    if ctx.fused && haskey(CHAIN_STEPS, tables) && haskey(CHAIN_STEPS[tables], idx.batch)
+        st = CHAIN_STEPS[tables][idx.batch]
+        st.dt === δ1.dt && return _fused_update!(opt, st, tables)
+    end
     ix = get!(() -> HipIndexer(ctx, length(tables), idx.batch * idx.lookups), INDEXERS, indexers)
     check(ctx, ccall((:dlrm_sgd_update, libdlrm), Cint,
                      (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cuint, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint,
@@ -381,6 +390,8 @@ mutable struct HipTrainStep{T}
     lr::Float32
     spare::Union{Nothing,HipIndexer}     # pipelined steps: the indexer the next batch is built into
     pending::Any                         # (next sparse => its packed indices) after train_step_bwd!(; next)
+    bwd::Symbol                          # operator chain: :none, :once_hit_applied, :all_dt, :done
+    delta::Union{Nothing,DeviceMatrix{T}}  # operator chain: the uploaded Δ of the pullback
 end
 function HipTrainStep(ctx::Context, tables::AbstractVector{<:HipEmbedding{Static{D},T}}, batch::Integer;
                       lr = 0.01, pad_to = 1) where {D,T}
@@ -389,7 +400,7 @@ function HipTrainStep(ctx::Context, tables::AbstractVector{<:HipEmbedding{Static
     return HipTrainStep{T}(ctx, collect(tables), HipIndexer(ctx, length(tables), batch),
                            DeviceMatrix{T}(ctx, width, batch), DeviceMatrix{Float32}(ctx, D, batch),
                            DeviceMatrix{Float32}(ctx, F * D, batch), nothing, nothing, padding, Float32(lr),
-                           nothing, nothing)
+                           nothing, nothing, :none, nothing)
 end
 
 function train_step_fwd!(st::HipTrainStep{T}, x::AbstractMatrix{T}, sparse) where {T}
@@ -441,6 +452,131 @@ function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}; next = noth
                         st.x.ptr, d, Δd.ptr, size(Δ, 1), st.padding, st.dx.ptr, d, st.dt.ptr, size(st.dt, 1),
                         st.lr, Cuint(0)))
     return Array(st.dx)
+end
+
+#####
+##### The unchanged operator chain on the step kernels (Python mirror: dlrm.jl_amd/lazy.py)
+#####
+# With `Context(dev; fused = true, lr = η)` the four calls an unchanged train! makes
+#   ys = maplookup(PreallocationStrategy(d), tables, sparse)      model.jl:161
+#   out = interaction(x, ys)  (+ its rrule pullback)                model.jl:163, interact.jl:438-447
+#   update!(Descent(η), tables, grads, indexers)                    train.jl:283-290
+# run the training-step pair: maplookup returns a HipLookup (nothing launched, ys never written),
+# the interaction on it is dlrm_step_fwd (gather + interaction + the update's indexer, one launch),
+# its pullback dlrm_step_bwd(DLRM_STEP_BWD_ONLY) (once-hit rows stepped with η there; without lr,
+# dlrm_interact_bwd_gather writes every dt row), and update! the apply launch.  Results are those of
+# the five-launch chain above, bit for bit (tests/test_gpu_parity.py, through the same ABI).
+
+const STEP_BWD_ONLY, STEP_APPLY_ONLY, UPDATE_PREBUILT = Cuint(1), Cuint(2), Cuint(2)
+
+"""
+    HipLookup
+
+`maplookup(PreallocationStrategy(P), tables, sparse)` on a fused context: the (P + D·T) × B lookup
+output, not materialized.  `DeviceMatrix(ys)` gathers it (dlrm_maplookup) for any other consumer.
+"""
+struct HipLookup{T} <: AbstractMatrix{T}
+    tables::AbstractVector          # the model's own Vector{HipEmbedding} (keys the step state)
+    idx::PackedIndices
+    P::Int
+end
+Base.size(ys::HipLookup) = (ys.P + featuresize(first(ys.tables)) * length(ys.tables), ys.idx.batch)
+Base.getindex(::HipLookup, ::Int...) = error("HipLookup is not materialized; DeviceMatrix(ys) gathers it")
+DeviceMatrix(ys::HipLookup) = first(_maplookup(ys.tables, ys.idx, ys.P))
+
+# one preallocated step state per (table set, batch size): out, dx, dt and the step's indexer
+const CHAIN_STEPS = IdDict{Any,Dict{Int,Any}}()
+chain_step(tables, B::Int) =
+    get!(() -> HipTrainStep(first(tables).data.ctx, tables, B; lr = something(first(tables).data.ctx.lr, 0f0)),
+         get!(() -> Dict{Int,Any}(), CHAIN_STEPS, tables), B)
+
+function _fused_maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse, P::Integer) where {D,T}
+    ctx = first(tables).data.ctx
+    idx = sparse isa PackedIndices ? sparse : pack(ctx, sparse)
+    return HipLookup{T}(tables, idx, Int(P))
+end
+
+function _fused_interact(dot::HipDotInteraction, x::AbstractMatrix{T}, ys::HipLookup{T}) where {T}
+    d, B = size(x)
+    d == ys.P || throw(DimensionMismatch("x has $d rows, maplookup reserved $(ys.P)"))
+    st = chain_step(ys.tables, B)
+    train_step_fwd!(st, x isa DeviceMatrix ? x : Matrix{T}(x), ys.idx)   # dlrm_step_fwd
+    st.bwd = :none
+    return st
+end
+
+(dot::HipDotInteraction)(x::AbstractMatrix{T}, ys::HipLookup{T}; return_t = false) where {T} =
+    return_t ? dot(x, DeviceMatrix(ys); return_t) : Array(_fused_interact(dot, x, ys).out)
+(dot::HipDotInteraction)(x::OneDNN.Memory, ys::HipLookup; kw...) = dot(OneDNN.materialize(x), ys; kw...)
+
+function ChainRulesCore.rrule(dot::HipDotInteraction, X, ys::HipLookup{T}) where {T}
+    x = X isa OneDNN.Memory ? OneDNN.materialize(X) : X
+    st = _fused_interact(dot, x, ys)
+    function dot_pullback(Δ)
+        Δh = Δ isa OneDNN.Memory ? OneDNN.materialize(Δ) : Δ
+        d, B = size(st.x)
+        st.delta = upload!(DeviceMatrix{T}(st.ctx, size(Δh)...), Matrix{T}(Δh))
+        if st.ctx.lr !== nothing   # once-hit rows stepped here, the others' dt rows left for update!
+            check(st.ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
+                                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid},
+                                 Int64, Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat, Cuint),
+                                st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch,
+                                1, B, st.x.ptr, d, st.delta.ptr, size(Δh, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                                size(st.dt, 1), st.ctx.lr, STEP_BWD_ONLY))
+            st.bwd = :once_hit_applied
+        else                       # every dt row written (T re-gathered, no ys)
+            check(st.ctx, ccall((:dlrm_interact_bwd_gather, libdlrm), Cint,
+                                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint,
+                                 Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64),
+                                st.ctx.ptr, tableset(st.tables), C_NULL, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1,
+                                B, 1, st.x.ptr, d, st.delta.ptr, size(Δh, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                                size(st.dt, 1)))
+            st.bwd = :all_dt
+        end
+        return (NoTangent(), Array(st.dx), st.dt)
+    end
+    return Array(st.out), dot_pullback
+end
+
+function ChainRulesCore.rrule(
+    ::typeof(maplookup), strategy::PreallocationStrategy, tables::AbstractVector{<:HipEmbedding{Static{D}}}, sparse
+) where {D}
+    first(tables).data.ctx.fused || return _rrule_maplookup(strategy, tables, sparse)
+    P = prealloc_rows(strategy)
+    ys = _fused_maplookup(tables, sparse, P)
+    function maplookup_pullback(dt)
+        dt isa DeviceMatrix{Float32} || throw(ArgumentError("the cotangent of ys is the dt of HipDotInteraction's pullback"))
+        ups = [SparseEmbeddingUpdate{Static{D}}(HipDelta(dt, P + (t - 1) * D, D), HipIndices(ys.idx, t))
+               for t in eachindex(tables)]
+        return (NoTangent(), NoTangent(), ups, NoTangent())
+    end
+    return ys, maplookup_pullback
+end
+
+# update! of a fused step: the apply launch (the grads are views of that step's dt)
+function _fused_update!(opt, st, tables)
+    ctx = st.ctx
+    d, B = size(st.x)
+    if st.bwd === :once_hit_applied
+        opt.eta == ctx.lr || throw(ArgumentError("the pullback stepped the once-hit rows with η = $(ctx.lr), update! got $(opt.eta)"))
+        check(ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
+                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
+                          Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat, Cuint),
+                         ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
+                         st.x.ptr, d, st.delta.ptr, size(st.delta, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                         size(st.dt, 1), ctx.lr, STEP_APPLY_ONLY))
+    elseif st.bwd === :all_dt         # the forward's split indexer: once-hit rows as singles items
+        check(ctx, ccall((:dlrm_sgd_update, libdlrm), Cint,
+                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cuint, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint,
+                          Ptr{Cvoid}, Cint, Int64, Int64, Cfloat),
+                         ctx.ptr, tableset(st.tables), st.ix.ptr, UPDATE_PREBUILT, st.idx.data.ptr, DLRM_I32,
+                         st.idx.batch, 1, st.idx.batch, 1, st.dt.ptr, DLRM_F32, size(st.dt, 1), d, opt.eta))
+    else
+        throw(ArgumentError("update! before the interaction's pullback ran"))
+    end
+    st.bwd = :done
+    check_bounds(ctx)
+    return nothing
 end
 
 #####

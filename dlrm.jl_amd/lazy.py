@@ -1,0 +1,181 @@
+"""The reference's operator chain on the fused training-step kernels.
+
+An unchanged `train!` (src/train/train.jl:215-227, :283-290) drives the hot path as four operators:
+
+    ys = maplookup(PreallocationStrategy(d), tables, sparse)     model.jl:161
+    out, back = rrule(interaction, x, ys)                          model.jl:163, interact.jl:438-447
+    _, dx, dy = back(Δ)                                            (Zygote pullback)
+    update!(Descent(η), tables, maplookup_pullback(dy), indexers)  train.jl:283-290
+
+Run literally, that is five launches with ys written to and read back from HBM.  `HipTables` is
+the table type whose methods make the same four calls hit the fused kernels (the Python mirror of
+DLRMHip.jl's lazy `maplookup` for `HipEmbedding`):
+
+  maplookup            -> a `LazyLookup` (indices + tables; nothing launched, ys never written)
+  DotInteraction(x, ys)-> dlrm_step_fwd: the gather, the interaction and the update's indexer in
+                          one launch (the gather-only forward)
+  its pullback         -> dlrm_step_bwd(DLRM_STEP_BWD_ONLY): dot_back on re-gathered rows; with the
+                          learning rate known up front (`HipTables(..., lr=η)`) the rows hit once in
+                          the batch get their SGD step right there, else every dt row is written
+  maplookup_pullback   -> `DeferredUpdate` views of that dt
+  update!              -> dlrm_step_bwd(DLRM_STEP_APPLY_ONLY) (the repeated rows), or, without a
+                          known η, dlrm_sgd_update(PREBUILT) with the forward's split indexer
+
+Three launches per step, bit for bit the result of `HotPath.step` and of the five-launch chain.
+Anything else that reads ys gets it materialized (`LazyLookup.materialize`).  `out`, `dx` and the
+gradient live in per-batch-size buffers reused by the next step, as the reference's own
+preallocated scratch (`DotInteraction`'s per-thread scratchpads) is.
+"""
+from . import _lib
+from .embedding import EmbeddingTableSet, PackedIndices, PreallocationStrategy, as_table_set
+from .update import Descent, SparseEmbeddingUpdate
+
+
+class HipTables:
+    """Vector{HipEmbedding{Static{D}}}: embedding tables whose lookup is deferred into the
+    interaction.  lr: the Descent η the following update! will use (lets the backward apply the
+    once-hit rows itself, the fastest form); None: update! applies every row."""
+
+    def __init__(self, tables, *, lr=None, index_base=0):
+        self.ts = as_table_set(tables) if not isinstance(tables, EmbeddingTableSet) else tables
+        self.lr = None if lr is None else float(lr)
+        self.index_base = int(index_base)
+        self._hp = {}
+
+    def __len__(self):
+        return len(self.ts)
+
+    def __iter__(self):
+        return iter(self.ts)
+
+    def __getitem__(self, i):
+        return self.ts[i]
+
+    @property
+    def D(self):
+        return self.ts.D
+
+    def hotpath(self, batch):
+        """The preallocated step state of one batch size (buffers, indexer)."""
+        from .hotpath import HotPath
+        hp = self._hp.get(batch)
+        if hp is None:
+            hp = HotPath(self.ts, batch, 1, lr=0.0 if self.lr is None else self.lr, index_base=self.index_base)
+            if not hp.step_api:
+                raise ValueError("HipTables: this table set has no training-step kernels (deterministic, one-hot)")
+            self._hp[batch] = hp
+        return hp
+
+
+class LazyLookup:
+    """maplookup(PreallocationStrategy(P), ::HipTables, sparse) before anything is gathered."""
+
+    def __init__(self, tables, idx, prealloc):
+        self.tables, self.idx, self.prealloc = tables, idx, int(prealloc)
+
+    @property
+    def shape(self):
+        return (self.idx.B, self.prealloc + self.tables.D * len(self.tables))
+
+    @property
+    def dtype(self):
+        return self.tables.ts.dtype
+
+    @property
+    def device(self):
+        return self.tables.ts.device
+
+    def materialize(self, check_bounds=True):
+        """The ys the reference's maplookup returns (one dlrm_maplookup launch)."""
+        from .embedding import maplookup
+        return maplookup(PreallocationStrategy(self.prealloc), self.tables.ts, self.idx,
+                         index_base=self.tables.index_base, check_bounds=check_bounds)
+
+    # -- the interaction on it: dlrm_step_fwd
+    def interact(self, x):
+        if x.shape[1] != self.prealloc:
+            raise ValueError(f"the interaction's x has {x.shape[1]} columns, maplookup reserved {self.prealloc}")
+        hp = self.tables.hotpath(self.idx.B)
+        hp.validate(x, self.idx)
+        hp.step_fwd(x, self.idx)
+        return hp
+
+
+class LazyGrad:
+    """The cotangent of a LazyLookup: the step backward's dt ([B][F*D] fp32, x rows first) and
+    whether the once-hit rows were already stepped (then only the repeated rows' dt rows exist)."""
+
+    def __init__(self, hp, idx, x, delta, applied_once_hit):
+        self.hp, self.idx, self.x, self.delta, self.applied = hp, idx, x, delta, applied_once_hit
+
+    @property
+    def dt(self):
+        return self.hp.dt
+
+
+class DeferredUpdate(SparseEmbeddingUpdate):
+    """One table's SparseEmbeddingUpdate from a LazyGrad: a view of dt like maplookup_pullback's,
+    plus the step state update! finishes."""
+
+    def __init__(self, lazy, table_index, prealloc):
+        hp = lazy.hp
+        super().__init__(hp.dt, prealloc + table_index * hp.D, hp.D, lazy.idx, table_index)
+        self.lazy = lazy
+
+    def uncompress(self, nrows, *, index_base=1):
+        if self.lazy.applied:
+            raise ValueError("the pullback stepped the once-hit rows itself (HipTables(lr=...)): dt holds only the "
+                             "repeated rows; build HipTables without lr to read the full gradient")
+        return super().uncompress(nrows, index_base=index_base)
+
+
+def maplookup_lazy(strategy, tables, sparse):
+    idx = PackedIndices(sparse, device=tables.ts.device)
+    if idx.T != len(tables):
+        raise ValueError(f"{idx.T} index arrays for {len(tables)} tables")
+    if isinstance(strategy, PreallocationStrategy) and idx.L == 1:
+        return LazyLookup(tables, idx, strategy.prealloc)
+    # pooled bags / DefaultStrategy: the plain operator (no fused step form)
+    from .embedding import maplookup
+    return maplookup(strategy, tables.ts, idx, index_base=tables.index_base)
+
+
+def rrule_lazy(x, ys):
+    """rrule(::DotInteraction, x, ::LazyLookup) -> (out, pullback)."""
+    hp = ys.interact(x)
+    tables, idx = ys.tables, ys.idx
+
+    def dot_pullback(delta):
+        if tables.lr is not None:  # once-hit rows stepped here (w = fmaf(-η, g, w)), the rest left in dt
+            hp.step_bwd(delta, x=x, idx=idx, flags=_lib.STEP_BWD_ONLY)
+        else:                      # every dt row written; update! steps every row
+            hp.interact_bwd(delta, x=x, idx=idx)
+        return None, hp.dx, LazyGrad(hp, idx, x, delta, tables.lr is not None)
+
+    return hp.out, dot_pullback
+
+
+def pullback_lazy(strategy_prealloc, tables, dy):
+    if dy.hp is not tables.hotpath(dy.idx.B):
+        raise ValueError("the gradient belongs to another table set")
+    return [DeferredUpdate(dy, t, strategy_prealloc) for t in range(len(tables))]
+
+
+def update_lazy(opt, tables, grads, *, check_bounds=True):
+    """update!(Descent(η), ::HipTables, grads): the apply launch of the step."""
+    if not isinstance(opt, Descent):
+        raise TypeError("update_ implements Descent (plain SGD), the optimizer DLRM.jl trains with")
+    lz = grads[0].lazy
+    if len(grads) != len(tables) or any(g.lazy is not lz or g.table_index != t for t, g in enumerate(grads)):
+        raise ValueError("update_ expects the per-table views of one maplookup pullback")
+    hp = lz.hp
+    if lz.applied:
+        if opt.eta != tables.lr:
+            raise ValueError(f"the pullback stepped the once-hit rows with η = {tables.lr}; update! got {opt.eta}")
+        hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY)
+    else:
+        hp.lr = opt.eta
+        hp.sgd_update(lz.idx, prebuilt=True)  # the forward's split indexer: once-hit rows as singles items
+    if check_bounds:
+        hp.check_bounds()
+    return tables

@@ -72,7 +72,13 @@ class SparseEmbeddingUpdate:
 
 def maplookup_pullback(strategy_prealloc, tables, sparse, dy):
     """Pullback of maplookup(PreallocationStrategy(P), tables, sparse) given dy [B][P + D*T]
-    (e.g. dt_reshaped from dot_back): views, no arithmetic (the rows 1:P belong to x)."""
+    (e.g. dt_reshaped from dot_back): views, no arithmetic (the rows 1:P belong to x).
+    HipTables + the LazyGrad of the fused interaction's pullback: DeferredUpdate views (lazy.py)."""
+    from .lazy import HipTables, LazyGrad, pullback_lazy
+    if isinstance(tables, HipTables) and isinstance(dy, LazyGrad):
+        return pullback_lazy(strategy_prealloc, tables, dy)
+    if isinstance(tables, HipTables):
+        tables = tables.ts
     ts = as_table_set(tables)
     idx = PackedIndices(sparse, device=ts.device)
     return [SparseEmbeddingUpdate(dy, strategy_prealloc + t * ts.D, ts.D, idx, t) for t in range(len(ts))]
@@ -146,6 +152,11 @@ def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, ind
     are accepted for signature parity; the GPU decomposition is chunk-based.
     Tables are mutated in place."""
     del num_splits, nthreads
+    from .lazy import DeferredUpdate, HipTables, update_lazy
+    if isinstance(tables, HipTables) and grads and isinstance(grads[0], DeferredUpdate):
+        return update_lazy(opt, tables, grads, check_bounds=check_bounds)
+    if isinstance(tables, HipTables):
+        tables = tables.ts
     if not isinstance(opt, Descent):
         raise TypeError("update_ implements Descent (plain SGD), the optimizer DLRM.jl trains with")
     ts = as_table_set(tables)

@@ -607,6 +607,49 @@ def test_prepare_with_unaligned_x_updates_once_hit_rows(pkg, gpu):
         np.testing.assert_allclose(to_np_f32(a.data), to_np_f32(b.data), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("rows,D,B,lr_known", [
+    ("kaggle", 128, 2048, True), ("kaggle", 128, 2048, False),   # the BASELINE metric shape
+    ([3, 4000, 9, 200000, 12], 16, 512, True), ([3, 4000, 9, 200000, 12], 16, 512, False)])
+def test_drop_in_operator_chain_on_step_kernels(pkg, gpu, rows, D, B, lr_known):
+    """The reference's unchanged operator chain (maplookup -> rrule(DotInteraction) -> pullback ->
+    maplookup_pullback -> update!) on HipTables runs the training-step kernels (3 launches, ys never
+    written) and equals HotPath.step bit for bit: out, dx, every table, over two steps."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    rng = np.random.default_rng(B + D)
+    T = len(rows)
+    tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
+    idxs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+            for _ in range(2)]
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    lr = 0.25
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr if lr_known else None)
+    dot = pkg.DotInteraction()
+    for p in idxs:
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p)
+        assert isinstance(ys, pkg.LazyLookup) and ys.shape == (B, D + T * D)
+        out, back = pkg.rrule(dot, x, ys)
+        _, dx, dy = back(dout)
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), index_base=0)
+    torch.cuda.synchronize()
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=0)
+    for p in idxs:
+        hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_f32(out), to_np_f32(hp.out))
+    assert np.array_equal(to_np_f32(dx), to_np_f32(hp.dx))
+    for a, b in zip(ht.ts, hp.ts):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+    if lr_known:  # the pullback stepped the once-hit rows with η: update! must use the same η
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, idxs[0])
+        _, back = pkg.rrule(dot, x, ys)
+        _, _, dy = back(dout)
+        with pytest.raises(ValueError):
+            pkg.update_(pkg.Descent(lr * 2), ht, pkg.maplookup_pullback(D, ht, idxs[0], dy), index_base=0)
+
+
 def test_step_api_state_and_bounds(pkg, gpu):
     """The forward's split indexer also drives the plain update (once-hit rows included, bit for
     bit the update of a fresh build); step_bwd needs step_fwd's indices; an out-of-range index
