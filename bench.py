@@ -65,11 +65,10 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=-1,
                     help="where the step's indexer is built: 0 in the forward's launch; 2 inside the previous "
                          "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 the next "
-                         "batch's indexer on a side stream during the step; -1 (default): 2 for rows of <= 256 B "
-                         "(the forward is the indexer's length: D=16 measured 67.1M vs 58.7M samples/s with 0, "
-                         "Terabyte bf16 x 128 45.6M vs 41.9M), 1 for "
-                         "one-hot batches > 2048 (no in-launch indexer: configs[2] 73.8M vs 71.7M), else 0 (the "
-                         "gather is the forward's length: D=128 49.0M vs 47.7M with 2)")
+                         "batch's indexer on a side stream during the step; -1 (default, pkg.step_pipeline): 2 for "
+                         "one-hot batches <= 2048 (round 3: the gather-only forward is shorter than the in-launch "
+                         "build; D=128 49.1M vs 43.8M samples/s with 0, D=16 72.6M), 1 for one-hot batches > 2048 "
+                         "(configs[2] 73.8M vs 71.7M), 0 for pooled bags")
     return ap.parse_args()
 
 

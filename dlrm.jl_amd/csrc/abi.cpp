@@ -392,7 +392,7 @@ int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, const void* i
               "dlrm_lookup_interact_fwd: leading dimensions too small");
     CHECK_ARG(batch == 0 || (x && out), "dlrm_lookup_interact_fwd: null buffer");
     rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
-                                    index_base, lookups, d, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
+                                    index_base, lookups, d, batch, x, x_ld, ys, ys_ld, out, out_ld, padding, tb->h_desc.data());
     if (rc != DLRM_E_UNSUPPORTED) return rc;
     if (!ys)
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
@@ -491,7 +491,7 @@ int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer*
     if (ix) ix->dev.vshift = 0;
     rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                     index_base, lookups, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld,
-                                    ix ? &ix->dev : nullptr);
+                                    ix ? &ix->dev : nullptr, tb->h_desc.data());
     if (rc || !ix) return rc;
     // as dlrm_indexer_build: a following update may pass DLRM_UPDATE_PREBUILT
     record_build(ix, false, indices, itype, table_stride, index_base, batch, lookups);
@@ -513,7 +513,7 @@ int dlrm_interact_bwd_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* 
               "dlrm_interact_bwd_blocked: null buffer");
     return launch_interact_bwd_blocked(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
                                        index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dst, dst_base,
-                                       dst_ld);
+                                       dst_ld, tb->h_desc.data());
 }
 
 // --------------------------------------------------------------------------- indexer
@@ -770,14 +770,14 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         // built by the previous step's apply launch (dlrm_step_bwd_prepare): the gather alone
         ix->prepared = false;
         rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
-                                        index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding);
+                                        index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding, tb->h_desc.data());
         if (rc != DLRM_E_UNSUPPORTED) return rc;  // (no fused forward for this x: build below)
     }
     ix->prepared = false;
     ix->built = false;
     ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? step_parts_log2() : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
-                         batch, x, x_ld, out, out_ld, padding, ix->dev);
+                         batch, x, x_ld, out, out_ld, padding, ix->dev, tb->h_desc.data());
     if (rc == DLRM_OK) {
         record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
         return DLRM_OK;
@@ -790,7 +790,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         // indexer in LDS (one 1024-thread workgroup per table)
         rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype,
                                         table_stride, index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld,
-                                        padding);
+                                        padding, tb->h_desc.data());
         if (rc == DLRM_OK)
             rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base,
                                       batch, 1, true, nullptr);
@@ -819,7 +819,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
         if (rc) return rc;
         rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype,
                                         table_stride, index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld,
-                                        padding);
+                                        padding, tb->h_desc.data());
         const int rj = ctx_hip(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0), "hipStreamWaitEvent(main)");
         if (rc == DLRM_E_UNSUPPORTED)
             return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
@@ -830,7 +830,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     }
     // no single-launch form for this shape: the fused forward, then the (unsplit) indexer
     rc = launch_lookup_interact_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
-                                    index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding);
+                                    index_base, 1, d, batch, x, x_ld, nullptr, 0, out, out_ld, padding, tb->h_desc.data());
     if (rc == DLRM_E_UNSUPPORTED)
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED,
                         "dlrm_step_fwd: no fused forward for this shape (16-B aligned rows and x, F <= 96 needed)");
@@ -864,11 +864,11 @@ static int step_bwd_impl(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const
         CHECK_ARG((uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && dx_ld % 4 == 0 && dt_ld % 4 == 0,
                   "dlrm_step_bwd: dx and dt must be 16-B aligned with leading dimensions divisible by 4");
         rc = launch_step_bwd(ctx, tb->d_desc, tb->T, tb->dtype, indices, itype, table_stride, index_base, d, batch, x,
-                             x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, ix->dev, lr);
+                             x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, ix->dev, lr, tb->h_desc.data());
         if (rc == DLRM_OK) ix->singles_done = true;
     } else {
         rc = launch_interact_bwd_gather(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride,
-                                        index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, nullptr);
+                                        index_base, 1, d, batch, x, x_ld, dout, dout_ld, dx, dx_ld, dt, dt_ld, nullptr, tb->h_desc.data());
     }
     if (rc || (flags & DLRM_STEP_BWD_ONLY)) return rc;
     // once-hit rows: updated by the split backward, else by this apply (an unsplit indexer lists

@@ -15,6 +15,9 @@ struct __attribute__((aligned(16))) TableDesc {
     int64_t nrows;
 };
 
+// Up to kArgTables table pointers travel by value in a forward kernel's arguments (TabPtrs).
+constexpr int kArgTables = 32;
+
 // Device-side error word: bit 0 = an out-of-range index was skipped.
 constexpr unsigned kErrIndex = 1u;
 
@@ -238,22 +241,27 @@ int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld,
-                               int padding);
+                               int padding,
+    const TableDesc* htabs = nullptr);
 int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
-                               int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix);
+                               int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix,
+    const TableDesc* htabs = nullptr);
 int launch_interact_bwd_blocked(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
                                 const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                 const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
-                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld);
+                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld,
+    const TableDesc* htabs = nullptr);
 int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype, const void* idx,
                     int itype, int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, void* out,
-                    int64_t out_ld, int padding, const IndexerDev& ix);
+                    int64_t out_ld, int padding, const IndexerDev& ix,
+    const TableDesc* htabs = nullptr);
 int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T, int dtype, const void* idx, int itype,
                     int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, const void* dout,
                     int64_t dout_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev& ix,
-                    float lr);
+                    float lr,
+    const TableDesc* htabs = nullptr);
 int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* dout, int64_t dout_ld,
                         const void* t, int64_t t_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld);
 int64_t hix_table_slots(int64_t cap);

@@ -83,6 +83,24 @@ struct GatherArgs {
     const int64_t* dtl;
 };
 
+// The descriptors of up to kArgTables tables by value, as a kernel argument (the fused forward
+// for F <= 32): a lane's row address then waits on its index load alone, and the pointer is read
+// with the kernel-argument base in SGPRs (tools/fwd_probe.hip bisect: 12.0 -> 10.9 us).
+struct TabPtrs {
+    const void* p[kArgTables];
+    uint32_t n[kArgTables];  // rows (every table here has < 2^32)
+};
+inline bool fill_tab_ptrs(TabPtrs& tp, const TableDesc* host, int T) {
+    if (!host || T <= 0 || T > kArgTables) return false;
+    for (int t = 0; t < T; ++t) {
+        if (host[t].nrows >= (int64_t)UINT32_MAX) return false;
+        tp.p[t] = host[t].data;
+        tp.n[t] = (uint32_t)host[t].nrows;
+    }
+    for (int t = T; t < kArgTables; ++t) { tp.p[t] = nullptr; tp.n[t] = 0; }
+    return true;
+}
+
 // A zero row: the source of padding rows (16NB > F) and of rows whose index is out of range, so
 // that every row load of the one-hot forward is an unconditional, unmasked load.
 constexpr int kZeroElems = 1024;  // fp32 elements (4 KB); column offsets wrap modulo this
@@ -105,11 +123,14 @@ static __device__ __attribute__((aligned(16))) float g_zero_row[kZeroElems];
 template <typename T, int NB> struct FwdPart {
     static constexpr int NT = NB * (NB + 1) / 2;  // lower-triangle tiles
 };
-template <typename T, int NB, bool FUSED, int WPB, int DC = 0, int WPS = 1, bool CONTIG = false>
+// TP: the table pointers / row counts from a TabPtrs kernel argument (else from ga.tabs).
+// DEFER: raise the bounds flag after the stores instead of where the index is checked.
+template <typename T, int NB, bool FUSED, int WPB, int DC = 0, int WPS = 1, bool CONTIG = false, bool TP = false,
+          bool DEFER = false>
 __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* stage_all, int d_, int F, int B,
                                                 const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys,
                                                 int64_t ys_ld, T* __restrict__ out, int64_t out_ld, int padding,
-                                                const GatherArgs& ga) {
+                                                const GatherArgs& ga, const TabPtrs* tp = nullptr) {
     const int d = DC > 0 ? DC : d_;
     typedef Frag<T> FR;
     typedef typename FR::type frag;
@@ -132,6 +153,7 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
     f32x4_t* xch = (f32x4_t*)(stage_all + SPB * kStage) + pair * NT * 64;
     const T* zero = (const T*)g_zero_row;
     constexpr int ZMASK = kZeroElems * 4 / (int)sizeof(T) - 1;
+    bool bad_any = false;  // an out-of-range index was skipped (zero row) by this lane
     for (int64_t b0 = (int64_t)bid * SPB; b0 < B; b0 += (int64_t)nblocks * SPB) {
         const int64_t bs = b0 + pair;
         const bool live = bs < B;
@@ -149,7 +171,8 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
             for (int I = 0; I < NB; ++I) {
                 const int row = I * 16 + c;
                 const bool tab = row >= 1 && row < F;
-                td[I] = load_table(ga.tabs, tab ? row - 1 : 0);
+                if constexpr (TP) td[I] = TableDesc{(void*)tp->p[tab ? row - 1 : 0], (int64_t)tp->n[tab ? row - 1 : 0]};
+                else td[I] = load_table(ga.tabs, tab ? row - 1 : 0);
                 ri[I] = load_index_if(tab, ga.idx, ga.itype, tab ? (row - 1) * ga.tstride + b : 0);
             }
             bool bad = false;
@@ -162,7 +185,8 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
                 bad |= tab & !ok;
                 src[I] = row == 0 ? xb : (ok ? (const T*)td[I].data + r * d : nullptr);
             }
-            if (bad & (q == 0) & (h == 0) & live) raise_index_error(ga.err);
+            if constexpr (DEFER) bad_any |= bad & (q == 0) & (h == 0) & live;
+            else if (bad & (q == 0) & (h == 0) & live) raise_index_error(ga.err);
         } else {
 #pragma unroll
             for (int I = 0; I < NB; ++I) {
@@ -291,6 +315,7 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
         }
         if (h == 0) WT(0, 2, b);
     }
+    if (DEFER && bad_any) raise_index_error(ga.err);
 }
 
 }  // namespace dlrm

@@ -60,16 +60,27 @@ extern "C" int dlrm_debug_wtrace(unsigned long long* out) {
 namespace dlrm {
 
 // Workgroup `bid` of `nblocks` (WPB waves, one sample per wave); stage_all = WPB * kStage floats of LDS.
+// The fused one-hot forward of F <= 32 features reads its table pointers from a TabPtrs kernel
+// argument (fwd_onehot.hpp); kDeferRaise: its bounds flag is raised after the stores.
+#ifndef DLRM_DEFER_RAISE
+#define DLRM_DEFER_RAISE 1
+#endif
+constexpr bool kDeferRaise = DLRM_DEFER_RAISE;
+template <int NB, bool FUSED, bool POOL> constexpr bool fwd_tab_ptrs() { return FUSED && !POOL && NB <= 2; }
+
 template <typename T, int NB, bool FUSED, int WPB, bool POOL = false, int DC = 0>
 __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all, int d_, int F, int B,
                                          const T* __restrict__ x, int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
-                                         T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga) {
+                                         T* __restrict__ out, int64_t out_ld, int padding, const GatherArgs& ga,
+                                         const TabPtrs* tp = nullptr) {
     // !POOL: one lookup per (table, sample) -- the callers pick the POOL kernel for FUSED, L > 1
     if constexpr (!POOL) {
-        // two waves per sample at the BASELINE feature size (d = 128: 4 fp32 / 2 bf16 column steps each)
-        constexpr int WPS = (DC == 128 && NB <= 2 && WPB % 2 == 0) ? 2 : 1;
-        fwd_body_onehot<T, NB, FUSED, WPB, DC, WPS>(bid, nblocks, stage_all, d_, F, B, x, x_ld, ys, ys_ld, out,
-                                                    out_ld, padding, ga);
+        // one wave per sample: with the table pointers in the kernel arguments it beats two waves per
+        // sample (column halves) at d = 128 -- tools/fwd_probe.hip: 10.5 vs 11.9 us
+        constexpr int WPS = 1;
+        constexpr bool TP = fwd_tab_ptrs<NB, FUSED, POOL>();
+        fwd_body_onehot<T, NB, FUSED, WPB, DC, WPS, false, TP, kDeferRaise && TP>(
+            bid, nblocks, stage_all, d_, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga, tp);
         return;
     }
     const int d = DC > 0 ? DC : d_;  // DC: the feature size as a compile-time constant
@@ -222,10 +233,10 @@ template <typename T, int NB, bool FUSED, bool POOL, int DC = 0, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                    int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                                                    T* __restrict__ out, int64_t out_ld, int padding,
-                                                                   GatherArgs ga) {
+                                                                   GatherArgs ga, TabPtrs tp) {
     __shared__ __attribute__((aligned(16))) float stage_all[WPB * kStage];
     fwd_body<T, NB, FUSED, WPB, POOL, DC>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding,
-                                ga);
+                                ga, &tp);
 }
 
 // The forward of a training step with the SparseIndexer build in the same grid (split form:
@@ -238,7 +249,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F,
 template <typename T, int NB, int DC = 0>
 __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                  int64_t x_ld, T* __restrict__ out, int64_t out_ld,
-                                                                 int padding, GatherArgs ga, IndexerDev ix) {
+                                                                 int padding, GatherArgs ga, IndexerDev ix,
+                                                                 TabPtrs tp) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int T_ = F - 1;
     const int NI = T_ << ix.vshift;
@@ -263,7 +275,7 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
         return;
     }
     fwd_body<T, NB, true, 4, false, DC>(blockIdx.x - NI, gridDim.x - NI, smem, d, F, B, x, x_ld, nullptr, 0, out,
-                                        out_ld, padding, ga);
+                                        out_ld, padding, ga, &tp);
 #ifdef DLRM_PHASE
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(&g_phase_fwd[61], wall_clock64());
@@ -841,31 +853,33 @@ static unsigned grid_for(int64_t items, int per_block, int cus) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
-// samples per 4-wave workgroup of the one-hot forward: two waves per sample at d = 128 (NB <= 2)
-static int fwd_samples_per_block(int d, int NB) { return (d == 128 && NB <= 2) ? 2 : 4; }
+// samples per 4-wave workgroup of the one-hot forward (fwd_body: one wave per sample)
+static int fwd_samples_per_block(int, int) { return 4; }
 
 template <typename T, int NB, bool FUSED>
 static void launch_fwd_nb(hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
-                          int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
+                          int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga,
+                          const TabPtrs& tp) {
     const bool pooled = FUSED && ga.L > 1;
     const unsigned g = grid_for(B, pooled ? 4 : fwd_samples_per_block(d, NB), cus);
     if (FUSED && ga.L > 1)
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, true>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
-                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga, tp);
     else if (d == 128)  // the BASELINE feature size, compiled for it
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, false, 128>), dim3(g), dim3(256), 0, s, d, F, B,
-                           (const T*)x, x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+                           (const T*)x, x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga, tp);
     else
         hipLaunchKernelGGL((interact_fwd_kernel<T, NB, FUSED, false>), dim3(g), dim3(256), 0, s, d, F, B, (const T*)x,
-                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga);
+                           x_ld, (T*)ys, ys_ld, (T*)out, out_ld, padding, ga, tp);
 }
 
 template <typename T, bool FUSED>
 static bool dispatch_fwd(int NB, hipStream_t s, int cus, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
-                         int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga) {
+                         int64_t ys_ld, void* out, int64_t out_ld, int padding, const GatherArgs& ga,
+                         const TabPtrs& tp = TabPtrs{}) {
     switch (NB) {
 #define DLRM_CASE(N) \
-    case N: launch_fwd_nb<T, N, FUSED>(s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga); return true;
+    case N: launch_fwd_nb<T, N, FUSED>(s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga, tp); return true;
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(3) DLRM_CASE(4) DLRM_CASE(5) DLRM_CASE(6)
 #undef DLRM_CASE
         default: return false;
@@ -909,7 +923,8 @@ int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, void* ys, int64_t ys_ld, void* out, int64_t out_ld,
-                               int padding) {
+                               int padding,
+                    const TableDesc* htabs) {
     if (B == 0) return DLRM_OK;
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
@@ -921,9 +936,11 @@ int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
+    TabPtrs tp{};
+    if (L == 1 && NB <= 2 && !fill_tab_ptrs(tp, htabs, T_)) return DLRM_E_UNSUPPORTED;  // (the two-launch form)
     const bool ok = dtype == DLRM_F32
-                        ? dispatch_fwd<float, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga)
-                        : dispatch_fwd<uint16_t, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga);
+                        ? dispatch_fwd<float, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga, tp)
+                        : dispatch_fwd<uint16_t, true>(NB, s, cus, d, F, B, x, x_ld, ys, ys_ld, out, out_ld, padding, ga, tp);
     if (!ok) return DLRM_E_UNSUPPORTED;
     return ctx_hip(ctx, hipGetLastError(), "lookup_interact_fwd launch");
 }
@@ -996,7 +1013,8 @@ int launch_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const voi
 int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
                                const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
-                               int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix) {
+                               int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev* ix,
+                    const TableDesc* htabs) {
     GatherArgs ga{tabs, idx, itype, tstride, base, L, ctx_error_word(ctx)};
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
@@ -1039,7 +1057,8 @@ int launch_interact_bwd_gather(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_a
 int launch_interact_bwd_blocked(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype,
                                 const void* idx, int itype, int64_t tstride, int base, int L, int d, int B,
                                 const void* x, int64_t x_ld, const void* dout, int64_t dout_ld, float* dx,
-                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld) {
+                                int64_t dx_ld, float* dst, const int64_t* dbase, const int64_t* dld,
+                    const TableDesc* htabs) {
     if (B == 0 || T_ == 0) return DLRM_OK;
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
@@ -1090,7 +1109,8 @@ bool step_split_supported(bool tabs_aligned16, int T_, int dtype, int d, const v
 // has no such kernel (the caller then runs the fused forward and the indexer separately).
 int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T_, int dtype, const void* idx,
                     int itype, int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, void* out,
-                    int64_t out_ld, int padding, const IndexerDev& ix) {
+                    int64_t out_ld, int padding, const IndexerDev& ix,
+                    const TableDesc* htabs) {
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;
     if (B == 0 || T_ == 0 || !tabs_aligned16 || !fwd_aligned(dtype, d, x, x_ld, nullptr, 0) || NB > 2 ||
@@ -1099,16 +1119,18 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
     hipStream_t s = ctx_stream(ctx);
     const int cus = ctx_num_cus(ctx);
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
+    TabPtrs tp{};
+    if (!fill_tab_ptrs(tp, htabs, T_)) return DLRM_E_UNSUPPORTED;
     size_t lds = sizeof(StepLds);
     if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
     const unsigned g = grid_for(B, fwd_samples_per_block(d, NB), cus) + (T_ << ix.vshift);
 #define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
     if (d == 128)                                                                                                  \
         hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_, 128>), dim3(g), dim3(256), lds, s, d, F, B,            \
-                           (const TY*)x, x_ld, (TY*)out, out_ld, padding, ga, ix);                                   \
+                           (const TY*)x, x_ld, (TY*)out, out_ld, padding, ga, ix, tp);                               \
     else                                                                                                           \
         hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_>), dim3(g), dim3(256), lds, s, d, F, B, (const TY*)x,   \
-                           x_ld, (TY*)out, out_ld, padding, ga, ix);
+                           x_ld, (TY*)out, out_ld, padding, ga, ix, tp);
     if (dtype == DLRM_F32) {
         if (NB == 1) DLRM_LAUNCH_FWDIX(float, 1) else DLRM_LAUNCH_FWDIX(float, 2)
     } else {
@@ -1124,7 +1146,8 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
 int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, const void* idx, int itype,
                     int64_t tstride, int base, int d, int B, const void* x, int64_t x_ld, const void* dout,
                     int64_t dout_ld, float* dx, int64_t dx_ld, float* dt, int64_t dt_ld, const IndexerDev& ix,
-                    float lr) {
+                    float lr,
+                    const TableDesc* htabs) {
     if (B == 0 || T_ == 0) return DLRM_OK;
     const int F = T_ + 1;
     const int NB = (F + 15) / 16;

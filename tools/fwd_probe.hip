@@ -117,24 +117,27 @@ __global__ void fill_random(float* p, int64_t n, uint32_t seed) {
 
 
 // The shipped one-hot body (dlrm.jl_amd/csrc/fwd_onehot.hpp), instantiated here with its knobs.
-template <int WPS, bool CONTIG, int WPB>
+template <int WPS, bool CONTIG, int WPB, bool TP, bool DEFER>
 __global__ __launch_bounds__(64 * WPB, 2) void libbody(int d, int F, int B, const float* __restrict__ x, int64_t x_ld,
                                                       float* __restrict__ out, int64_t out_ld, int padding,
-                                                      dlrm::GatherArgs ga) {
+                                                      dlrm::GatherArgs ga, dlrm::TabPtrs tp) {
     __shared__ __attribute__((aligned(16))) float stage_all[WPB * dlrm::kStage];
-    dlrm::fwd_body_onehot<float, 2, true, WPB, 128, WPS, CONTIG>(blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld,
-                                                                 nullptr, 0, out, out_ld, padding, ga);
+    dlrm::fwd_body_onehot<float, 2, true, WPB, 128, WPS, CONTIG, TP, DEFER>(
+        blockIdx.x, gridDim.x, stage_all, d, F, B, x, x_ld, nullptr, 0, out, out_ld, padding, ga, &tp);
 }
 
-template <int WPS, bool CONTIG, int WPB>
-double run_body(const dlrm::TableDesc* dtabs, const int* idx, const float* x, float* out, unsigned* err) {
+template <int WPS, bool CONTIG, int WPB, bool TP = false, bool DEFER = false>
+double run_body(const dlrm::TableDesc* dtabs, const int* idx, const float* x, float* out, unsigned* err,
+                const dlrm::TableDesc* htabs = nullptr) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int grid = B / (WPB / WPS);
     auto go = [&](int i) {
         dlrm::GatherArgs ga{dtabs, idx + (size_t)(i % NBATCH) * T * B, 0, B, 0, 1, err, nullptr, nullptr};
-        hipLaunchKernelGGL((libbody<WPS, CONTIG, WPB>), dim3(grid), dim3(64 * WPB), 0, 0, D, F, B, x, (int64_t)D, out,
-                           (int64_t)W, 1, ga);
+        dlrm::TabPtrs tp{};
+        if (TP) dlrm::fill_tab_ptrs(tp, htabs, T);
+        hipLaunchKernelGGL((libbody<WPS, CONTIG, WPB, TP, DEFER>), dim3(grid), dim3(64 * WPB), 0, 0, D, F, B, x,
+                           (int64_t)D, out, (int64_t)W, 1, ga, tp);
     };
     for (int i = 0; i < NBATCH; ++i) go(i);
     const int reps = 4 * NBATCH;
@@ -404,7 +407,7 @@ int main() {
     std::mt19937_64 g(1);
     dlrm_ctx* ctx = nullptr;
     if (dlrm_ctx_create(0, nullptr, &ctx)) { printf("ctx\n"); return 1; }
-    for (int cfg = 1; cfg < 3; ++cfg) {
+    for (int cfg = 1; cfg < 2; ++cfg) {
         const int layout = cfg == 2;       // 0, 1: Kaggle rows; 2: every table 10.1M rows
         const bool randomize = cfg >= 1;   // table contents: zeros (cfg 0) or random
         // layout 0: Kaggle rows; 1: every table 10.1M rows (all rows random in HBM)
@@ -443,6 +446,10 @@ int main() {
             CK(hipMemcpy(dtabs, hd.data(), T * sizeof(dlrm::TableDesc), hipMemcpyHostToDevice));
             printf("%s body wps2 interleaved %7.2f us\n", lname, run_body<2, false, 4>(dtabs, idx, x, out, err));
             printf("%s body wps2 contiguous  %7.2f us\n", lname, run_body<2, true, 4>(dtabs, idx, x, out, err));
+            printf("%s body wps2 TabPtrs     %7.2f us\n", lname, run_body<2, false, 4, true>(dtabs, idx, x, out, err, hd.data()));
+            printf("%s body wps2 defer raise %7.2f us\n", lname, run_body<2, false, 4, false, true>(dtabs, idx, x, out, err, hd.data()));
+            printf("%s body wps2 TabPtrs+defer%6.2f us\n", lname, run_body<2, false, 4, true, true>(dtabs, idx, x, out, err, hd.data()));
+            printf("%s body wps1 TabPtrs+defer%6.2f us\n", lname, run_body<1, false, 4, true, true>(dtabs, idx, x, out, err, hd.data()));
             printf("%s body wps2 contig wpb8 %7.2f us\n", lname, run_body<2, true, 8>(dtabs, idx, x, out, err));
             printf("%s body wps1             %7.2f us\n", lname, run_body<1, false, 4>(dtabs, idx, x, out, err));
             float* zf;
