@@ -44,7 +44,7 @@ def parse():
                          "weak scaling, the workload's batch per GPU")
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
-                         "0: the engine's default (2 where a rank's batch is >= 256)")
+                         "0: the engine's default (1: DESIGN.md §6)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

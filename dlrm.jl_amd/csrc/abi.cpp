@@ -292,7 +292,7 @@ int dlrm_maplookup(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, in
               "dlrm_maplookup: out_ld %lld < out_offset %lld + T*D %lld", (long long)out_ld, (long long)out_offset,
               (long long)tb->T * tb->D);
     return launch_maplookup(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype, table_stride,
-                            index_base, batch, lookups, out, out_ld, out_offset);
+                            index_base, batch, lookups, out, out_ld, out_offset, tb->h_desc.data());
 }
 
 int dlrm_maplookup_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* indices, int itype,
@@ -306,7 +306,8 @@ int dlrm_maplookup_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* ind
               "dlrm_maplookup_blocked: negative stride or block_rows < 1");
     return launch_maplookup_map(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype,
                                 table_stride, index_base, batch, lookups, out,
-                                OutMap{out_ld, out_offset, out_table_stride, block_rows, block_stride});
+                                OutMap{out_ld, out_offset, out_table_stride, block_rows, block_stride},
+                                tb->h_desc.data());
 }
 
 int dlrm_scatter_rows(dlrm_ctx* ctx, int esize, int num_tables, int batch, int dim, const void* src, int64_t src_ld,
@@ -399,7 +400,7 @@ int dlrm_lookup_interact_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, const void* i
                         "dlrm_lookup_interact_fwd: ys may be NULL only where the fused kernel applies "
                         "(16-B aligned rows, F <= 96)");
     rc = launch_maplookup(ctx, tb->d_desc, tb->aligned16, tb->T, tb->D, tb->dtype, indices, itype, table_stride,
-                          index_base, batch, lookups, ys, ys_ld, d);
+                          index_base, batch, lookups, ys, ys_ld, d, tb->h_desc.data());
     if (rc) return rc;
     return launch_interact_fwd(ctx, tb->dtype, d, F, batch, x, x_ld, ys, ys_ld, out, out_ld, padding);
 }

@@ -155,6 +155,29 @@ __device__ __forceinline__ void store_row(TT* row, int c0, const float* f) {
     }
 }
 
+// The descriptors of up to kArgTables tables by value, as a kernel argument (the one-hot forward,
+// the lookup): a lane's row address then waits on its index load alone, and the pointer is read
+// with the kernel-argument base in SGPRs (tools/fwd_probe.hip bisect: 12.0 -> 10.9 us).
+struct TabPtrs {
+    const void* p[kArgTables];
+    uint32_t n[kArgTables];  // rows (every table here has < 2^32)
+};
+inline bool fill_tab_ptrs(TabPtrs& tp, const TableDesc* host, int T) {
+    if (!host || T <= 0 || T > kArgTables) return false;
+    for (int t = 0; t < T; ++t) {
+        if (host[t].nrows >= (int64_t)UINT32_MAX) return false;
+        tp.p[t] = host[t].data;
+        tp.n[t] = (uint32_t)host[t].nrows;
+    }
+    for (int t = T; t < kArgTables; ++t) { tp.p[t] = nullptr; tp.n[t] = 0; }
+    return true;
+}
+
+// A zero row: the source of padding rows (16NB > F) and of rows whose index is out of range, so
+// that every row load of the one-hot forward and of the lookup is an unconditional, unmasked load.
+constexpr int kZeroElems = 1024;  // fp32 elements (4 KB); column offsets wrap modulo this
+static __device__ __attribute__((aligned(16))) float g_zero_row[kZeroElems];
+
 }  // namespace dlrm
 
 namespace dlrm {
@@ -235,7 +258,7 @@ int ctx_device(dlrm_ctx* ctx);
 
 int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                      const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
-                     int64_t out_ld, int64_t out_off);
+                     int64_t out_ld, int64_t out_off, const TableDesc* htabs = nullptr);
 int launch_interact_fwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const void* x, int64_t x_ld, void* ys,
                         int64_t ys_ld, void* out, int64_t out_ld, int padding);
 int launch_lookup_interact_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, int T, int dtype,
@@ -270,7 +293,7 @@ int launch_hix_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs,
 bool step_split_supported(bool tabs_aligned16, int T, int dtype, int d, const void* x, int64_t x_ld);
 int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                          const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
-                         const OutMap& om);
+                         const OutMap& om, const TableDesc* htabs = nullptr);
 int launch_dac_decode(dlrm_ctx* ctx, const void* rec, int B, float* labels, float* dense, int64_t dense_ld,
                       void* sparse, int itype, int64_t tstride);
 int launch_bce_head(dlrm_ctx* ctx, int B, const float* z, int64_t z_ld, const float* y, float* prob, float* dz,

@@ -83,29 +83,6 @@ struct GatherArgs {
     const int64_t* dtl;
 };
 
-// The descriptors of up to kArgTables tables by value, as a kernel argument (the fused forward
-// for F <= 32): a lane's row address then waits on its index load alone, and the pointer is read
-// with the kernel-argument base in SGPRs (tools/fwd_probe.hip bisect: 12.0 -> 10.9 us).
-struct TabPtrs {
-    const void* p[kArgTables];
-    uint32_t n[kArgTables];  // rows (every table here has < 2^32)
-};
-inline bool fill_tab_ptrs(TabPtrs& tp, const TableDesc* host, int T) {
-    if (!host || T <= 0 || T > kArgTables) return false;
-    for (int t = 0; t < T; ++t) {
-        if (host[t].nrows >= (int64_t)UINT32_MAX) return false;
-        tp.p[t] = host[t].data;
-        tp.n[t] = (uint32_t)host[t].nrows;
-    }
-    for (int t = T; t < kArgTables; ++t) { tp.p[t] = nullptr; tp.n[t] = 0; }
-    return true;
-}
-
-// A zero row: the source of padding rows (16NB > F) and of rows whose index is out of range, so
-// that every row load of the one-hot forward is an unconditional, unmasked load.
-constexpr int kZeroElems = 1024;  // fp32 elements (4 KB); column offsets wrap modulo this
-static __device__ __attribute__((aligned(16))) float g_zero_row[kZeroElems];
-
 // One-hot forward (L = 1): every row load of a column block (all UU x NB fragments) is issued
 // before the first MFMA, so a wave keeps its whole share of the sample's rows in flight at once.
 // The compiler's own schedule interleaved one load, a wait and its MFMAs (one 1-KB load in flight

@@ -17,63 +17,85 @@
 
 namespace dlrm {
 
-// KB lookups of a bag are fetched per round: their indices first (independent loads), then
-// U x KB rows in flight, then accumulated in k order -- a pooled bag costs ceil(L / KB)
-// index->row round trips instead of L.
-template <typename T, int VPR, int U, int KB>
-__global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict__ tabs, int ntab,
+// A wave takes RPW*U consecutive (sample, table) items; per round of KB lookups of a bag every
+// index load of its U bags is issued first, then every row load (unmasked: an out-of-range index
+// reads the zero row and raises the flag after the stores), then the k-ordered sums -- a lane
+// keeps U x KB x VPL 16-B loads in flight, and a bag costs ceil(L / KB) index->row round trips.
+// (The branchy form waited on each row load before issuing the next: 23 us for the sharded
+// lookup's 65,536 rows of 512 B.)  TP: the table pointers from a TabPtrs argument (T <= 32),
+// else one descriptor load per item, issued with the first round's index loads.
+#ifndef DLRM_LOOKUP_NT
+#define DLRM_LOOKUP_NT 0
+#endif
+constexpr bool kLookupNT = DLRM_LOOKUP_NT;  // non-temporal output stores (A/B builds)
+template <typename T, int VPR, int U, int KB, bool TP>
+__global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict__ tabs, TabPtrs tp, int ntab,
                                                      const void* __restrict__ idx, int itype,
                                                      int64_t tstride, int base, int B, int L,
                                                      T* __restrict__ out, OutMap om, unsigned* __restrict__ err) {
     typedef Vec<T> V;
+    typedef typename V::type vt;
     constexpr int NE = V::N;                       // elements per 16-B vector
     constexpr int LPR = VPR <= 64 ? VPR : 64;      // lanes per row
     constexpr int VPL = VPR <= 64 ? 1 : VPR / 64;  // vectors per lane
     constexpr int RPW = 64 / LPR;                  // rows per wave-instruction
+    static_assert(VPR * 16 <= kZeroElems * 4, "rows longer than the zero row");
     const int lane = threadIdx.x & 63;
     const int g = lane / LPR, v = lane % LPR;
     if (g >= RPW) return;  // idle lanes when LPR does not divide 64
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const int64_t total = (int64_t)ntab * B;
+    const int wave = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nwaves = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
+    const int total = ntab * B;  // < 2^31 (launch_maplookup_map)
     constexpr int D = VPR * NE;
+    const vt* zero = (const vt*)g_zero_row;
+    bool bad = false;
 
-    for (int64_t first = wave * (RPW * U); first < total; first += nwaves * (RPW * U)) {
-        int64_t bb[U];
-        int tt[U];
+    for (int first = wave * (RPW * U); first < total; first += nwaves * (RPW * U)) {
+        int bb[U], tt[U];
         bool live[U];
-        float acc[U][VPL][NE];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t item = first + u * RPW + g;
+            const int item = first + u * RPW + g;
             live[u] = item < total;
-            bb[u] = item / ntab;
-            tt[u] = (int)(item - bb[u] * ntab);
+            const int it = live[u] ? item : 0;
+            bb[u] = it / ntab;
+            tt[u] = it - bb[u] * ntab;
         }
+        TableDesc td[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (TP) td[u] = TableDesc{(void*)tp.p[tt[u]], (int64_t)tp.n[tt[u]]};
+            else td[u] = load_table(tabs, tt[u]);
+        }
+        float acc[U][VPL][NE];
         for (int k0 = 0; k0 < L; k0 += KB) {
-            int64_t r[U][KB];
+            int64_t ri[U][KB];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int kk = 0; kk < KB; ++kk)
-                    r[u][kk] = load_index_if(live[u] && k0 + kk < L, idx, itype,
-                                             tt[u] * tstride + bb[u] * L + k0 + kk) - base;
-            typename V::type vv[U][KB][VPL];
+                    ri[u][kk] = load_index_if(live[u] && k0 + kk < L, idx, itype,
+                                              tt[u] * tstride + (int64_t)bb[u] * L + k0 + kk);
+            const vt* src[U][KB];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int kk = 0; kk < KB; ++kk) {
-                    const T* rowp = nullptr;
-                    if (live[u] && k0 + kk < L) {
-                        if (r[u][kk] >= 0 && r[u][kk] < tabs[tt[u]].nrows) rowp = (const T*)tabs[tt[u]].data + r[u][kk] * D;
-                        else if (v == 0) raise_index_error(err);
-                    }
-#pragma unroll
-                    for (int j = 0; j < VPL; ++j) {
-                        if (rowp) vv[u][kk][j] = *((const typename V::type*)(rowp) + v + j * 64);
-                        else vv[u][kk][j] = typename V::type{};
-                    }
+                    const bool use = live[u] && k0 + kk < L;
+                    const int64_t r = ri[u][kk] - base;
+                    const bool ok = use & (r >= 0) & (r < td[u].nrows);
+                    bad |= use & !ok;
+                    src[u][kk] = ok ? (const vt*)((const T*)td[u].data + r * D) : zero;
                 }
+            __builtin_amdgcn_sched_barrier(0);
+            vt vv[U][KB][VPL];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+                    for (int j = 0; j < VPL; ++j) vv[u][kk][j] = ldg<vt>(src[u][kk] + v + j * 64);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -93,9 +115,13 @@ __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict
             if (!live[u]) continue;
             T* o = out + om.row(bb[u]) + (int64_t)tt[u] * om.tstride;
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) *((typename V::type*)o + v + j * 64) = V::from_f32(acc[u][j]);
+            for (int j = 0; j < VPL; ++j) {
+                if constexpr (kLookupNT) stg_nt<vt>((vt*)o + v + j * 64, V::from_f32(acc[u][j]));
+                else stg<vt>((vt*)o + v + j * 64, V::from_f32(acc[u][j]));
+            }
         }
     }
+    if (bad && v == 0) raise_index_error(err);
 }
 
 // Scalar fallback for shapes / alignments the vector kernel does not take.
@@ -124,31 +150,37 @@ __global__ __launch_bounds__(256) void maplookup_scalar(const TableDesc* __restr
 }
 
 template <typename T, int VPR>
-static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx, int itype,
-                       int64_t tstride, int base, int B, int L, void* out, const OutMap& om, unsigned* err) {
+static void launch_vec(hipStream_t s, int cus, const TableDesc* tabs, const TabPtrs* tp, int T_, const void* idx,
+                       int itype, int64_t tstride, int base, int B, int L, void* out, const OutMap& om, unsigned* err) {
     constexpr int LPR = VPR <= 64 ? VPR : 64;
     constexpr int RPW = 64 / LPR;
-    const int U = L > 1 ? 2 : 4;  // pooled: 2 bags x 4 lookups in flight per lane group
+    // one-hot: 4 rows per lane group (8 at <= 256-B rows); pooled: 2 bags x 4 lookups
+    constexpr int U1 = VPR <= 16 ? 8 : 4;
+    const int U = L > 1 ? 2 : U1;
     const int64_t total = (int64_t)T_ * B;
     const int64_t waves = (total + RPW * U - 1) / (RPW * U);
     int64_t blocks = (waves + 3) / 4;
     const int64_t cap = (int64_t)cus * 16;  // grid-stride beyond 16 blocks per CU
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    if (L > 1)
-        hipLaunchKernelGGL((maplookup_vec<T, VPR, 2, 4>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx,
-                           itype, tstride, base, B, L, (T*)out, om, err);
-    else
-        hipLaunchKernelGGL((maplookup_vec<T, VPR, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s, tabs, T_, idx,
-                           itype, tstride, base, B, L, (T*)out, om, err);
+    static const TabPtrs none{};
+#define DLRM_LAUNCH(U_, KB_, TP_)                                                                               \
+    hipLaunchKernelGGL((maplookup_vec<T, VPR, U_, KB_, TP_>), dim3((unsigned)blocks), dim3(256), 0, s, tabs,       \
+                       tp ? *tp : none, T_, idx, itype, tstride, base, B, L, (T*)out, om, err)
+    if (L > 1) {
+        if (tp) DLRM_LAUNCH(2, 4, true); else DLRM_LAUNCH(2, 4, false);
+    } else {
+        if (tp) DLRM_LAUNCH(U1, 1, true); else DLRM_LAUNCH(U1, 1, false);
+    }
+#undef DLRM_LAUNCH
 }
 
 template <typename T>
-static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs, int T_, const void* idx,
-                         int itype, int64_t tstride, int base, int B, int L, void* out, const OutMap& om,
-                         unsigned* err) {
+static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs, const TabPtrs* tp, int T_,
+                         const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
+                         const OutMap& om, unsigned* err) {
 #define DLRM_CASE(N) \
-    case N: launch_vec<T, N>(s, cus, tabs, T_, idx, itype, tstride, base, B, L, out, om, err); return true;
+    case N: launch_vec<T, N>(s, cus, tabs, tp, T_, idx, itype, tstride, base, B, L, out, om, err); return true;
     switch (vpr) {
         DLRM_CASE(1) DLRM_CASE(2) DLRM_CASE(4) DLRM_CASE(8) DLRM_CASE(16) DLRM_CASE(32) DLRM_CASE(64)
         DLRM_CASE(128) DLRM_CASE(256)
@@ -159,14 +191,14 @@ static bool dispatch_vec(int vpr, hipStream_t s, int cus, const TableDesc* tabs,
 
 int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T_, int D, int dtype,
                      const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
-                     int64_t out_ld, int64_t out_off) {
+                     int64_t out_ld, int64_t out_off, const TableDesc* htabs) {
     return launch_maplookup_map(ctx, d_tabs, tabs_aligned16, T_, D, dtype, idx, itype, tstride, base, B, L, out,
-                                OutMap{out_ld, out_off, D, B > 0 ? B : 1, 0});
+                                OutMap{out_ld, out_off, D, B > 0 ? B : 1, 0}, htabs);
 }
 
 int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T_, int D, int dtype,
                          const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
-                         const OutMap& om) {
+                         const OutMap& om, const TableDesc* htabs) {
     if (T_ == 0 || B == 0) return DLRM_OK;
     hipStream_t s = ctx_stream(ctx);
     unsigned* err = ctx_error_word(ctx);
@@ -176,11 +208,14 @@ int launch_maplookup_map(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_align
                          ((om.off * esz) % 16 == 0) && ((om.tstride * esz) % 16 == 0) &&
                          ((om.bstride * esz) % 16 == 0) && ((D * esz) % 16 == 0);
     bool done = false;
-    if (aligned) {
+    if (aligned && (int64_t)T_ * B < (1ll << 31)) {
         const int vpr = D * esz / 16;
+        TabPtrs tp;
+        const TabPtrs* tpp = fill_tab_ptrs(tp, htabs, T_) ? &tp : nullptr;
         done = dtype == DLRM_F32
-                   ? dispatch_vec<float>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, om, err)
-                   : dispatch_vec<uint16_t>(vpr, s, cus, d_tabs, T_, idx, itype, tstride, base, B, L, out, om, err);
+                   ? dispatch_vec<float>(vpr, s, cus, d_tabs, tpp, T_, idx, itype, tstride, base, B, L, out, om, err)
+                   : dispatch_vec<uint16_t>(vpr, s, cus, d_tabs, tpp, T_, idx, itype, tstride, base, B, L, out, om,
+                                            err);
     }
     if (!done) {
         const int64_t total = (int64_t)T_ * B * D;

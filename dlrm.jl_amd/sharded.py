@@ -32,7 +32,9 @@ way moves the looked-up vectors to the ranks that own the samples, and their gra
 Per rank and step: lookup(m) for every m on the compute stream; exchange_fwd(m) on the comm stream
 as soon as lookup(m) is done; interaction fwd + bwd of m once its vectors arrived; exchange_bwd(m) on
 the comm stream; the update when the last gradient block arrived.  Exposed: the first forward and
-the last backward exchange (1/M of each direction) -- DESIGN.md §6.
+the last backward exchange (1/M of each direction) -- DESIGN.md §6.  M = 1 (the default): lookup,
+exchange, interaction, exchange and update in stream order on the compute stream, the index build
+alone on the side stream.
 
 All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-ABI kernels)
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
@@ -365,6 +367,17 @@ class ShardedHotPath:
         with torch.cuda.stream(self._side):
             index()
             self._ix_done.record(self._side)
+        if M == 1:
+            # nothing to overlap the exchanges with: they run in stream order on the compute
+            # stream (each cross-stream event hop costs a few us of dependency latency:
+            # tools/shard_sim.py, step 140 us against 68 us of main-stream work with four hops)
+            lookup(0)
+            self.exchange_fwd(0)
+            interact(0)
+            self.exchange_bwd(0)
+            main.wait_event(self._ix_done)
+            update()
+            return
         for m in range(M):
             lookup(m)
             ev_look[m].record(main)
@@ -420,11 +433,12 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
                       micro=None):
     """Bench setup for one rank: local tables (full size) and nbatch index batches for the
     global batch; returns (engine, step(k) closure, prepare_graphs() closure).  batch_local =
-    global batch / world for strong scaling.  micro: micro-batches per step (default: 2 where
-    the rank's batch splits into halves of >= 128 samples, else 1)."""
+    global batch / world for strong scaling.  micro: micro-batches per step (default 1: with two,
+    the per-micro-batch launches and cross-stream event hops cost more than the exchange overlap
+    hides -- tools/shard_sim.py at world 8: 185 us per step, launch-bound, against 103 us with one)."""
     import numpy as np
     if micro is None:
-        micro = 2 if batch_local % 2 == 0 and batch_local >= 256 else 1
+        micro = 1
     rows = w["rows"]
     D, L = w["dim"], w["lookups"]
     E = 4 if w["dtype"] == "f32" else 2

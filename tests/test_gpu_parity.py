@@ -93,6 +93,28 @@ def test_lookup_vs_oracle(pkg, gpu, dim, lookups, dtype):
     assert np.array_equal(to_np_bits(out)[:, P:], ref[:, P:])
 
 
+@pytest.mark.parametrize("ntab", [31, 33, 40])
+@pytest.mark.parametrize("lookups", [1, 5])
+def test_lookup_table_pointer_forms(pkg, gpu, ntab, lookups):
+    """<= 32 tables: pointers by value in the kernel arguments; more: descriptor loads (lookup.hip)."""
+    rng = np.random.default_rng(ntab * 7 + lookups)
+    rows = [int(r) for r in rng.integers(1, 3000, ntab)]
+    B = 203
+    tabs = rand_tables(rng, rows, 128)
+    idx = rand_indices(rng, rows, B, lookups)
+    dt = dev_tables(tabs, gpu)
+    out = pkg.maplookup(pkg.PreallocationStrategy(128), dt, torch.from_numpy(idx).reshape(ntab, B, lookups).to(gpu),
+                        index_base=0)
+    ref = np.zeros((B, 128 * (ntab + 1)), dtype=np.float32)
+    oracle.maplookup(tabs, idx, 0, B, lookups, ref, 128)
+    assert np.array_equal(to_np_f32(out)[:, 128:], ref[:, 128:])
+    bad = idx.copy().reshape(ntab, B * lookups)
+    bad[ntab - 1, B * lookups // 2] = rows[ntab - 1]  # one out-of-range index in the last table
+    with pytest.raises(pkg.BoundsError):
+        pkg.maplookup(pkg.PreallocationStrategy(128), dt, torch.from_numpy(bad).reshape(ntab, B, lookups).to(gpu),
+                      index_base=0)
+
+
 @pytest.mark.parametrize("itype", [torch.int32, torch.int64])
 @pytest.mark.parametrize("base", [0, 1])
 def test_lookup_index_types_and_base(pkg, gpu, itype, base):

@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import torch
 
@@ -63,11 +64,14 @@ def main():
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         s.record()
+        h0 = time.perf_counter()
         for k in range(a.iters):
             fn(k)
+        h1 = time.perf_counter()
         e.record()
         torch.cuda.synchronize()
         res[name] = round(s.elapsed_time(e) * 1e3 / a.iters, 2)
+        res["host_" + name] = round((h1 - h0) * 1e6 / a.iters, 2)  # launch-side time per replay
     res["main_stream"] = round(res["seg_lookup"] + res["seg_interact"] + res["seg_update"], 2)
     res["micro_batches"], res["batch_per_rank"] = M, B
     E = 4 if w["dtype"] == "f32" else 2
