@@ -369,7 +369,30 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     constexpr int SP = NG * G::SPPG;                           // positions per singles item
     const int per_t = SG ? (sa.N + SP - 1) / SP : 0;          // singles items per real table
     const int items = citems + (T_ >> ix.vshift) * per_t;
-    for (int item = bid; item < items; item += nblk) {
+    // Pooled bags (L > 1): every position of a bag reads the bag's gradient row, so a table's
+    // gradient slice ([B][D]: 2 MB at B = 2048, D = 256 fp32) is read about L times.  Workgroups b
+    // and b + 8 share an XCD (and its L2): with the plain stride every XCD walks every table and
+    // fetches each slice for itself.  Instead each XCD takes one contiguous eighth of each item
+    // kind (hot slices, chunk items, once-hit items) -- about an eighth of the tables -- so a slice
+    // is fetched by one L2 and re-read there.  (One-hot: each gradient row is read once; plain.)
+    //   item = pos + (pos < e0 ? r0 : pos < e1 ? s1 : s2), pos = this workgroup's list position
+    int pos0 = bid, step = nblk, npos = items, r0 = 0, e0 = items, s1 = 0, e1 = items, s2 = 0;
+    if (L > 1 && (nblk & 7) == 0 && ((blockIdx.x - bid) & 7) == 0) {
+        const int x = bid & 7, c1 = citems - sS.total, c2 = items - citems;
+        const int a0 = (int)((int64_t)sS.total * x >> 3), b0 = (int)((int64_t)sS.total * (x + 1) >> 3);
+        const int a1 = (int)((int64_t)c1 * x >> 3), b1 = (int)((int64_t)c1 * (x + 1) >> 3);
+        const int a2 = (int)((int64_t)c2 * x >> 3), b2 = (int)((int64_t)c2 * (x + 1) >> 3);
+        r0 = a0;
+        e0 = b0 - a0;
+        s1 = sS.total + a1 - e0;
+        e1 = e0 + (b1 - a1);
+        s2 = citems + a2 - e1;
+        npos = e1 + (b2 - a2);
+        pos0 = bid >> 3;
+        step = nblk >> 3;
+    }
+    for (int pos = pos0; pos < npos; pos += step) {
+        const int item = pos + (pos < e0 ? r0 : (pos < e1 ? s1 : s2));
         APPLY_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2));
         if (SG && item >= citems) {  // uniform: once-hit positions of one real table
             const int t = (item - citems) / per_t;
