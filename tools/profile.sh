@@ -20,3 +20,5 @@ timeout -k 10 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$
 python3 tools/prof_summary.py --kt "$O/kt" --fetch "$O/fetch" --write "$O/write" --mfma "$O/mfma" --workload "$WL" --head "${DLRM_HEAD:-unknown}" --out "$O/${TAG}_${WL}" || exit 1
 cp "$(find "$O/kt" -name '*kernel_stats.csv' | head -n 1)" "$O/${TAG}_${WL}_kernel_stats.csv"
 cp "$O/${TAG}_${WL}.json" "$O/pmc_${WL}.json"
+# the raw traces stay on the box (gpurun copies back at most 64 MiB)
+rm -rf "$O/kt" "$O/fetch" "$O/write" "$O/mfma"
