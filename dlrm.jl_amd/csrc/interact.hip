@@ -24,6 +24,7 @@
 // The interaction's arithmetic intensity (~11-24 flop/B) is far below the MFMA ridge, so
 // these kernels are HBM-bound; MFMA just keeps the VALU free and the operand traffic low.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -601,19 +602,28 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
 // are most of a small-d backward's time.
 // MAPPED (dlrm_interact_bwd_blocked): table rows' gradients go to the send layout (GatherArgs dtb /
 // dtl), none to dt's x row; a separate instantiation, so the step kernels keep their LDS budget.
-template <typename T, int NB, int DC, int SPB, int WPS = 2, bool MAPPED = false>
-__global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
+// CPL = 8 (bf16 rows): a lane loads 8 columns (16 B) of each row and runs 8 MFMAs per k-step, so
+// a super-block is 128 columns and one wave takes a d = 128 sample whole (half the load
+// instructions per byte of the 4-column form, and more samples resident per CU); the gathered
+// rows stay bf16 in the wave's LDS tile.  Every output element is the same MFMA sum over the same
+// k-steps as in the 4-column form: dx, dt and the tables are bit-identical.
+template <typename T, int NB, int DC, int SPB, int WPS = 2, bool MAPPED = false, int CPL = 4>
+__global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
                                                                    int64_t dout_ld, float* __restrict__ dx,
                                                                    int64_t dx_ld, float* __restrict__ dt,
                                                                    int64_t dt_ld, GatherArgs ga,
                                                                    const T* __restrict__ x, int64_t x_ld,
                                                                    StepUpdate su) {
+    static_assert(CPL == 4 || (CPL == 8 && sizeof(T) == 2), "8 columns per lane: bf16 rows");
     constexpr int NS = 16 * NB;
     constexpr int KS = 4 * NB;
     constexpr int PMAX = NS * (NS - 1) / 2;
+    constexpr int SBC = 16 * CPL;  // columns per super-block
+    // the wave's tile of T: fp32 (CPL = 4) or the rows' own bf16 (CPL = 8)
+    typedef typename std::conditional<CPL == 8, uint16_t, float>::type TileT;
     const int d = DC > 0 ? DC : d_;
     __shared__ float pk_all[SPB][PMAX];  // each sample's packed gradient row
-    __shared__ __attribute__((aligned(16))) float tt_all[WPS * SPB][NS * 64];  // each wave's 64-column tile of T
+    __shared__ __attribute__((aligned(16))) TileT tt_all[WPS * SPB][NS * SBC];  // each wave's tile of T
     __shared__ TableDesc tds[NS];
     __shared__ int64_t dmap[MAPPED ? 2 * NS : 1];  // table t's dt rows at dt + dmap[t] + b * dmap[F - 1 + t]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -627,7 +637,7 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
     const int P = F * (F - 1) / 2;
     const T* ob = dout + bb * dout_ld;
     float* pk = pk_all[pair];
-    float* Tt = tt_all[w];
+    TileT* Tt = tt_all[w];
     if (h == 0) WT(1, 0, b);
     // the table descriptors (F - 1 <= NS <= 32 < blockDim: one per thread), held in registers and
     // written to LDS after the other independent loads are issued, so no wave waits for them alone
@@ -651,14 +661,18 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
         const float v = to_f32(ldg<T>(ob + d + (p < P ? p : 0)));
         pv[k] = p < P ? v : 0.0f;
     }
-    // super-blocks per wave (WPS = 2: d <= 512 when not fixed; WPS = 1: d <= 64)
+    // super-blocks per wave (CPL = 4, WPS = 2: d <= 512 when not fixed; WPS = 1: d <= 64;
+    // CPL = 8: d <= 128, one wave)
     constexpr int SBW = WPS == 1 ? 1 : (DC > 0 ? (DC / 64 + 1) / 2 : 4);
-    float xv[SBW];
+    constexpr int XV = SBC / 64;  // dout x-part values per lane and super-block
+    float xv[SBW][XV];
 #pragma unroll
-    for (int sbi = 0; sbi < SBW; ++sbi) {
-        const int n = 64 * h + 64 * WPS * sbi + lane;
-        xv[sbi] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
-    }
+    for (int sbi = 0; sbi < SBW; ++sbi)
+#pragma unroll
+        for (int k = 0; k < XV; ++k) {
+            const int n = SBC * h + SBC * WPS * sbi + 64 * k + lane;
+            xv[sbi][k] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
+        }
     const bool frozen = *su.err != 0;  // a bounds error this step: no table row is written
     if (tdl_ok) {
         tds[threadIdx.x] = tdl;
@@ -690,7 +704,8 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
         const T* src = (s < ksteps && kk == 0) ? x + bb * x_ld
                                                : (tab ? (const T*)tds[kk - 1].data + (int64_t)r * d : nullptr);
         livek |= src ? (1u << s) : 0u;
-        rowp[s] = src ? src : ob;
+        // (CPL = 8: a masked row reads the zero row -- a 16-B aligned source whatever dout's layout)
+        rowp[s] = src ? src : (CPL == 8 ? (const T*)g_zero_row : ob);
     }
     uint32_t urow[NB][4];
 #pragma unroll
@@ -706,47 +721,88 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
     if (h == 0) WT(1, 1, b);
 #pragma unroll
     for (int sbi = 0; sbi < SBW; ++sbi) {
-        const int sb = 64 * h + 64 * WPS * sbi;
+        const int sb = SBC * h + SBC * WPS * sbi;
         if (sb >= d) break;
-        const int n0 = sb + 4 * c;  // this lane's 4 output columns
+        const int n0 = sb + CPL * c;  // this lane's CPL output columns
         const bool colok = n0 < d;
         const int nc = colok ? n0 : 0;
-        f32x4_t bv[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const f32x4_t v = load4_f32(rowp[s] + nc);
-            bv[s] = ((livek >> s) & 1u) && colok ? v : f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-        if (sbi > 0) wave_lds_sync();  // the previous super-block's tile reads are done
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-            if (s < ksteps) *(f32x4_t*)(Tt + (4 * s + q) * 64 + 4 * c) = bv[s];
-        f32x4_t acc[NB][4];
+        f32x4_t acc[NB][CPL];
 #pragma unroll
         for (int I = 0; I < NB; ++I)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            for (int e = 0; e < CPL; ++e) acc[I][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if constexpr (CPL == 4) {
+            f32x4_t bv[KS];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (s < ksteps) {
-                const int kk = 4 * s + q;
+            for (int s = 0; s < KS; ++s) {
+                const f32x4_t v = load4_f32(rowp[s] + nc);
+                bv[s] = ((livek >> s) & 1u) && colok ? v : f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+            if (sbi > 0) wave_lds_sync();  // the previous super-block's tile reads are done
 #pragma unroll
-                for (int I = 0; I < NB; ++I) {
-                    // S[16I+c][kk]: the symmetric zero-diagonal unpack of the pair row
-                    const int i = I * 16 + c;
-                    const int hi = i > kk ? i : kk, lo = i > kk ? kk : i;
-                    const float av = (i != kk && hi < F) ? pk[hi * (hi - 1) / 2 + lo] : 0.0f;
+            for (int s = 0; s < KS; ++s)
+                if (s < ksteps) *(f32x4_t*)(Tt + (4 * s + q) * SBC + 4 * c) = bv[s];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s][e], acc[I][e], 0, 0, 0);
+            for (int s = 0; s < KS; ++s) {
+                if (s < ksteps) {
+                    const int kk = 4 * s + q;
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) {
+                        // S[16I+c][kk]: the symmetric zero-diagonal unpack of the pair row
+                        const int i = I * 16 + c;
+                        const int hi = i > kk ? i : kk, lo = i > kk ? kk : i;
+                        const float av = (i != kk && hi < F) ? pk[hi * (hi - 1) / 2 + lo] : 0.0f;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[s][e], acc[I][e], 0, 0, 0);
+                    }
+                }
+            }
+        } else {
+            typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+            u32x4_t bv[KS];  // 8 bf16 columns of row 4s+q, packed
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const u32x4_t v = ldg<u32x4_t>(rowp[s] + nc);
+                bv[s] = ((livek >> s) & 1u) && colok ? v : u32x4_t{0u, 0u, 0u, 0u};
+            }
+            if (sbi > 0) wave_lds_sync();  // the previous super-block's tile reads are done
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                if (s < ksteps) *(u32x4_t*)(Tt + (4 * s + q) * SBC + 8 * c) = bv[s];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                if (s < ksteps) {
+                    const int kk = 4 * s + q;
+#pragma unroll
+                    for (int I = 0; I < NB; ++I) {
+                        const int i = I * 16 + c;
+                        const int hi = i > kk ? i : kk, lo = i > kk ? kk : i;
+                        const float av = (i != kk && hi < F) ? pk[hi * (hi - 1) / 2 + lo] : 0.0f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const uint32_t wd = bv[s][e >> 1];
+                            const float bvf = __uint_as_float((e & 1) ? (wd & 0xffff0000u) : (wd << 16));
+                            acc[I][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bvf, acc[I][e], 0, 0, 0);
+                        }
+                    }
                 }
             }
         }
         if (h == 0 && sbi == 0) WT(1, 2, b);
         // dout's x part for this lane's columns (lanes 0..15 hold output row 0)
-        f32x4_t xo;
+        float xo[CPL];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xo[e] = __shfl(xv[sbi], 4 * c + e, 64);
+        for (int e = 0; e < CPL; ++e) {
+            const int n = CPL * c + e;  // column within the super-block: lane n & 63 of xv[sbi][n >> 6]
+            float xs = __shfl(xv[sbi][0], n & 63, 64);
+#pragma unroll
+            for (int k = 1; k < XV; ++k) {
+                const float t = __shfl(xv[sbi][k], n & 63, 64);
+                xs = (n >> 6) == k ? t : xs;
+            }
+            xo[e] = xs;
+        }
         wave_lds_sync();  // the tile of T (written before the MFMAs)
         if (!live || !colok) continue;
 #pragma unroll
@@ -755,19 +811,41 @@ __global__ __launch_bounds__(64 * WPS * SPB, 4) void interact_bwd_split_kernel(i
             for (int r = 0; r < 4; ++r) {
                 const int f = I * 16 + 4 * q + r;
                 if (f < F) {
-                    const f32x4_t v = f32x4_t{acc[I][0][r], acc[I][1][r], acc[I][2][r], acc[I][3][r]};
-                    if (urow[I][r] != ~0u) {
-                        float wv[4];
-                        const f32x4_t tw = *(const f32x4_t*)(Tt + f * 64 + 4 * c);  // the row as gathered
+                    float v[CPL];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
-                        store_row<T, 4, true>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
+                    for (int e = 0; e < CPL; ++e) v[e] = acc[I][e][r];
+                    if (urow[I][r] != ~0u) {
+                        float wv[CPL];
+                        float tw[CPL];  // the row as gathered
+                        if constexpr (CPL == 4) {
+                            const f32x4_t t4 = *(const f32x4_t*)(Tt + f * SBC + 4 * c);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) tw[e] = t4[e];
+                        } else {
+                            typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+                            const u32x4_t t8 = *(const u32x4_t*)(Tt + f * SBC + 8 * c);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e)
+                                tw[e] = __uint_as_float((e & 1) ? (t8[e >> 1] & 0xffff0000u) : (t8[e >> 1] << 16));
+                        }
+#pragma unroll
+                        for (int e = 0; e < CPL; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
+                        store_row<T, CPL, true>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
                     } else if constexpr (!mapped) {
-                        stg_nt<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0, v);
+#pragma unroll
+                        for (int e = 0; e < CPL; e += 4)
+                            stg_nt<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0 + e, f32x4_t{v[e], v[e + 1], v[e + 2], v[e + 3]});
                     } else if (f > 0) {
-                        stg_nt<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0, v);
+#pragma unroll
+                        for (int e = 0; e < CPL; e += 4)
+                            stg_nt<f32x4_t>(dt + dmap[f - 1] + b * dmap[F - 2 + f] + n0 + e,
+                                            f32x4_t{v[e], v[e + 1], v[e + 2], v[e + 3]});
                     }
-                    if (f == 0) stg<f32x4_t>(dx + b * dx_ld + n0, xo + v);
+                    if (f == 0)
+#pragma unroll
+                        for (int e = 0; e < CPL; e += 4)
+                            stg<f32x4_t>(dx + b * dx_ld + n0 + e, f32x4_t{xo[e] + v[e], xo[e + 1] + v[e + 1],
+                                                                         xo[e + 2] + v[e + 2], xo[e + 3] + v[e + 3]});
                 }
             }
         if (h == 0 && sbi == 0) {
@@ -1161,10 +1239,10 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     static const bool split = !getenv("DLRM_BWD_SPLIT") || atoi(getenv("DLRM_BWD_SPLIT")) != 0;
     if (split && d == 128) {
         // samples per block (DLRM_BWD_SPB = 2, 4 or 8 overrides)
-        static const int spb = [] {
+        static const int spb_env = [] {
             const char* e = getenv("DLRM_BWD_SPB");
-            const int v = e ? atoi(e) : 4;
-            return v >= 8 ? 8 : (v >= 4 ? 4 : 2);
+            const int v = e ? atoi(e) : 0;
+            return v >= 8 ? 8 : (v >= 4 ? 4 : (v > 0 ? 2 : 0));
         }();
 #define DLRM_LAUNCH_SPLIT(TY, N_, S_)                                                                              \
     hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 128, S_>), dim3((unsigned)((B + S_ - 1) / S_)),            \
@@ -1174,11 +1252,27 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     if (spb == 8) DLRM_LAUNCH_SPLIT(TY, N_, 8);     \
     else if (spb == 4) DLRM_LAUNCH_SPLIT(TY, N_, 4); \
     else DLRM_LAUNCH_SPLIT(TY, N_, 2);
+        // bf16: 8 columns per lane, one wave per sample (DLRM_BWD_CPL = 4: the two-wave form);
+        // kaggle-d128-b8192-bf16 backward 52.2 -> 48.4 us with 2 samples per block (r6q)
+        static const bool cpl8 = !getenv("DLRM_BWD_CPL") || atoi(getenv("DLRM_BWD_CPL")) == 8;
+        const int spb = spb_env ? spb_env : (dtype != DLRM_F32 && cpl8 ? 2 : 4);
+#define DLRM_LAUNCH_SPLIT8(N_, S_)                                                                                 \
+    hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, N_, 128, S_, 1, false, 8>),                             \
+                       dim3((unsigned)((B + S_ - 1) / S_)), dim3(64 * S_), 0, s, d, F, B, (const uint16_t*)dout,    \
+                       dout_ld, dx, dx_ld, dt, dt_ld, ga, (const uint16_t*)x, x_ld, su)
+#define DLRM_LAUNCH_SPLIT8_S(N_)                 \
+    if (spb == 8) DLRM_LAUNCH_SPLIT8(N_, 8);     \
+    else if (spb == 4) DLRM_LAUNCH_SPLIT8(N_, 4); \
+    else DLRM_LAUNCH_SPLIT8(N_, 2);
         if (dtype == DLRM_F32) {
             if (NB == 1) { DLRM_LAUNCH_SPLIT_S(float, 1) } else { DLRM_LAUNCH_SPLIT_S(float, 2) }
+        } else if (cpl8) {
+            if (NB == 1) { DLRM_LAUNCH_SPLIT8_S(1) } else { DLRM_LAUNCH_SPLIT8_S(2) }
         } else {
             if (NB == 1) { DLRM_LAUNCH_SPLIT_S(uint16_t, 1) } else { DLRM_LAUNCH_SPLIT_S(uint16_t, 2) }
         }
+#undef DLRM_LAUNCH_SPLIT8_S
+#undef DLRM_LAUNCH_SPLIT8
 #undef DLRM_LAUNCH_SPLIT_S
 #undef DLRM_LAUNCH_SPLIT
         return ctx_hip(ctx, hipGetLastError(), "step_bwd(split) launch");
