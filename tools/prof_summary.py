@@ -9,8 +9,12 @@
   coalesced read stream, so HBM read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
   16-B stores.  hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 * MFMA pass (--pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, own run): mfma_busy = the MFMA busy
-  cycles summed over the chip / (1024 SIMDs x GRBM_GUI_ACTIVE cycles of the dispatch), i.e. the
-  fraction of SIMD-cycles the matrix cores were busy (north_star's MFMA utilisation).
+  cycles summed over the chip / (1024 SIMDs x the dispatch's cycles), i.e. the fraction of
+  SIMD-cycles the matrix cores were busy (north_star's MFMA utilisation).  rocprofv3 reports
+  GRBM_GUI_ACTIVE summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back), so the dispatch's
+  cycles are GRBM_GUI_ACTIVE / 8; it reads high on dispatches much shorter than 0.3 ms, so the
+  fraction is a lower bound there.
+  --refresh FILE.json recomputes mfma_busy of an existing summary and rewrites its .json / .md.
 Writes <out>.json (consumed by bench.py for roofline.traffic) and <out>.md.
 """
 import argparse
@@ -68,14 +72,19 @@ def counters(d, name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kt", required=True)
+    ap.add_argument("--kt")
+    ap.add_argument("--refresh", help="an existing summary .json: recompute mfma_busy, rewrite .json/.md")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--mfma")
     ap.add_argument("--head", default="unknown", help="git HEAD the profiled library was built from")
     ap.add_argument("--workload", default="kaggle-d128-b2048")
-    ap.add_argument("--out", required=True)
+    ap.add_argument("--out")
     a = ap.parse_args()
+    if a.refresh:
+        old = json.load(open(a.refresh))
+        finish(old["kernels"], old["workload"], old.get("head", "unknown"), a.out or a.refresh[:-len(".json")])
+        return
     kernels = {}
     for r in read_csv(one(a.kt, "*kernel_stats.csv")):
         if "dlrm::" not in r["Name"]:
@@ -100,7 +109,17 @@ def main():
         if m and g:
             v["MFMA_BUSY_CYCLES_avg"] = sum(m) / len(m)
             v["GRBM_GUI_ACTIVE_avg"] = sum(g) / len(g)
-            v["mfma_busy"] = v["MFMA_BUSY_CYCLES_avg"] / (1024.0 * v["GRBM_GUI_ACTIVE_avg"])
+    finish(kernels, a.workload, a.head, a.out)
+
+
+def busy(v):
+    return v["MFMA_BUSY_CYCLES_avg"] / (1024.0 * v["GRBM_GUI_ACTIVE_avg"] / 8.0)
+
+
+def finish(kernels, workload, head, out_path):
+    for v in kernels.values():
+        if "MFMA_BUSY_CYCLES_avg" in v and v.get("GRBM_GUI_ACTIVE_avg"):
+            v["mfma_busy"] = busy(v)
     stages = defaultdict(lambda: {"avg_us": 0.0, "kernels": []})
     for k, v in kernels.items():
         if v["stage"] is None:
@@ -112,18 +131,18 @@ def main():
             s["hbm_bytes_per_launch"] = s.get("hbm_bytes_per_launch", 0) + v["hbm_bytes_per_launch"]
         if "mfma_busy" in v:
             s["mfma_busy"] = max(s.get("mfma_busy", 0.0), v["mfma_busy"])
-    out = {"workload": a.workload, "head": a.head, "kernels": kernels, **{k: dict(v) for k, v in stages.items()}}
-    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
-    with open(a.out + ".json", "w") as f:
+    out = {"workload": workload, "head": head, "kernels": kernels, **{k: dict(v) for k, v in stages.items()}}
+    os.makedirs(os.path.dirname(os.path.abspath(out_path)), exist_ok=True)
+    with open(out_path + ".json", "w") as f:
         json.dump(out, f, indent=1)
-    lines = [f"# rocprofv3 summary — {a.workload} (library built at {a.head})", "",
+    lines = [f"# rocprofv3 summary — {workload} (library built at {head})", "",
              "| kernel | stage | calls | avg µs | min µs | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2·F+W) | MFMA busy |",
              "|---|---|---|---|---|---|---|---|---|"]
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_us"]):
         lines.append(f"| `{k}` | {v['stage']} | {v['calls']} | {v['avg_us']:.2f} | {v['min_us']:.2f} | "
                      f"{v.get('FETCH_SIZE_KB_avg', float('nan')):.0f} | {v.get('WRITE_SIZE_KB_avg', float('nan')):.0f} | "
                      f"{v.get('hbm_bytes_per_launch', '—')} | {v.get('mfma_busy', float('nan')):.3f} |")
-    with open(a.out + ".md", "w") as f:
+    with open(out_path + ".md", "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
