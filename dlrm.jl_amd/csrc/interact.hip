@@ -1252,10 +1252,13 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     if (spb == 8) DLRM_LAUNCH_SPLIT(TY, N_, 8);     \
     else if (spb == 4) DLRM_LAUNCH_SPLIT(TY, N_, 4); \
     else DLRM_LAUNCH_SPLIT(TY, N_, 2);
-        // bf16: 8 columns per lane, one wave per sample (DLRM_BWD_CPL = 4: the two-wave form);
-        // kaggle-d128-b8192-bf16 backward 52.2 -> 48.4 us with 2 samples per block (r6q)
-        static const bool cpl8 = !getenv("DLRM_BWD_CPL") || atoi(getenv("DLRM_BWD_CPL")) == 8;
-        const int spb = spb_env ? spb_env : (dtype != DLRM_F32 && cpl8 ? 2 : 4);
+        // bf16, B > 2048: 8 columns per lane, one wave per sample, 2 samples per block
+        // (kaggle-d128-b8192-bf16: backward 52.2 -> 48.4 us, step 110.9 -> 103.3 us, r6q; at B = 2048
+        // the two-wave form keeps the step shorter: Terabyte rows 50.6 vs 48.7 M samples/s, r6s).
+        // DLRM_BWD_CPL = 4 / 8 forces either form.
+        static const int cpl_env = getenv("DLRM_BWD_CPL") ? atoi(getenv("DLRM_BWD_CPL")) : 0;
+        const bool cpl8 = dtype != DLRM_F32 && (cpl_env ? cpl_env == 8 : B > 2048);
+        const int spb = spb_env ? spb_env : (cpl8 ? 2 : 4);
 #define DLRM_LAUNCH_SPLIT8(N_, S_)                                                                                 \
     hipLaunchKernelGGL((interact_bwd_split_kernel<uint16_t, N_, 128, S_, 1, false, 8>),                             \
                        dim3((unsigned)((B + S_ - 1) / S_)), dim3(64 * S_), 0, s, d, F, B, (const uint16_t*)dout,    \
