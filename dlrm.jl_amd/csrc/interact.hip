@@ -607,8 +607,12 @@ __global__ __launch_bounds__(256, 2) void interact_bwd_update_kernel(int d, int 
 // instructions per byte of the 4-column form, and more samples resident per CU); the gathered
 // rows stay bf16 in the wave's LDS tile.  Every output element is the same MFMA sum over the same
 // k-steps as in the 4-column form: dx, dt and the tables are bit-identical.
-template <typename T, int NB, int DC, int SPB, int WPS = 2, bool MAPPED = false, int CPL = 4>
-__global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
+// YS (dlrm_interact_bwd on a materialized ys, e.g. pooled bags): T row kk of sample b is ys row
+// x + b * x_ld + kk * d (x / x_ld carry ys / ys_ld), no index, flag or once-hit update; every dt row
+// is written.  Up to 96 features (NB <= 6): the gather-free backward of the pooled workload
+// (F = 65), one wave per 64-column super-block.
+template <typename T, int NB, int DC, int SPB, int WPS = 2, bool MAPPED = false, int CPL = 4, bool YS = false>
+__global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : (NB > 2 ? 2 : 4)) void interact_bwd_split_kernel(int d_, int F, int B, const T* __restrict__ dout,
                                                                    int64_t dout_ld, float* __restrict__ dx,
                                                                    int64_t dx_ld, float* __restrict__ dt,
                                                                    int64_t dt_ld, GatherArgs ga,
@@ -623,8 +627,9 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd
     typedef typename std::conditional<CPL == 8, uint16_t, float>::type TileT;
     const int d = DC > 0 ? DC : d_;
     __shared__ float pk_all[SPB][PMAX];  // each sample's packed gradient row
-    __shared__ __attribute__((aligned(16))) TileT tt_all[WPS * SPB][NS * SBC];  // each wave's tile of T
-    __shared__ TableDesc tds[NS];
+    // each wave's tile of T (the once-hit update reads it; YS has none)
+    __shared__ __attribute__((aligned(16))) TileT tt_all[YS ? 1 : WPS * SPB][YS ? 4 : NS * SBC];
+    __shared__ TableDesc tds[YS ? 1 : NS];
     __shared__ int64_t dmap[MAPPED ? 2 * NS : 1];  // table t's dt rows at dt + dmap[t] + b * dmap[F - 1 + t]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pair = w / WPS, h = w % WPS;
@@ -637,21 +642,21 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd
     const int P = F * (F - 1) / 2;
     const T* ob = dout + bb * dout_ld;
     float* pk = pk_all[pair];
-    TileT* Tt = tt_all[w];
+    TileT* Tt = tt_all[YS ? 0 : w];
     if (h == 0) WT(1, 0, b);
     // the table descriptors (F - 1 <= NS <= 32 < blockDim: one per thread), held in registers and
     // written to LDS after the other independent loads are issued, so no wave waits for them alone
-    const bool tdl_ok = (int)threadIdx.x < F - 1;
-    const TableDesc tdl = load_table(ga.tabs, tdl_ok ? (int)threadIdx.x : 0);
+    const bool tdl_ok = !YS && (int)threadIdx.x < F - 1;
+    const TableDesc tdl = YS ? TableDesc{nullptr, 0} : load_table(ga.tabs, tdl_ok ? (int)threadIdx.x : 0);
     int64_t dm0 = 0, dm1 = 0;
     if constexpr (MAPPED) {
         dm0 = ldg<int64_t>(ga.dtb + (tdl_ok ? threadIdx.x : 0));
         dm1 = ldg<int64_t>(ga.dtl + (tdl_ok ? threadIdx.x : 0));
     }
     // ---- every independent load first: table `lane`'s index and flag, the packed gradients, x part
-    const bool tl = lane < F - 1;
-    const int64_t myidx = load_index_if(tl, ga.idx, ga.itype, (int64_t)(tl ? lane : 0) * ga.tstride + bb);
-    // su.single NULL (dlrm_interact_bwd_blocked): no once-hit update, every table row goes to dt
+    const bool tl = !YS && lane < F - 1;
+    const int64_t myidx = YS ? 0 : load_index_if(tl, ga.idx, ga.itype, (int64_t)(tl ? lane : 0) * ga.tstride + bb);
+    // su.single NULL (dlrm_interact_bwd_blocked, YS): no once-hit update, every table row goes to dt
     const uint8_t myfl = su.single ? ldg<uint8_t>(su.single + (tl ? (int64_t)lane * su.cap + bb : 0)) : (uint8_t)0;
     constexpr int PPW = (PMAX + 64 * WPS - 1) / (64 * WPS);  // packed values staged per lane
     float pv[PPW];
@@ -663,7 +668,10 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd
     }
     // super-blocks per wave (CPL = 4, WPS = 2: d <= 512 when not fixed; WPS = 1: d <= 64;
     // CPL = 8: d <= 128, one wave)
-    constexpr int SBW = WPS == 1 ? 1 : (DC > 0 ? (DC / 64 + 1) / 2 : 4);
+    // (DC = 0: WPS = 1 / 2 cover d <= 64 / 512; YS: d = 64 * WPS, one super-block per wave)
+    constexpr int SBW = YS ? 1
+                           : DC > 0 ? ((DC / SBC + WPS - 1) / WPS > 0 ? (DC / SBC + WPS - 1) / WPS : 1)
+                                    : (WPS == 2 ? 4 : 1);
     constexpr int XV = SBC / 64;  // dout x-part values per lane and super-block
     float xv[SBW][XV];
 #pragma unroll
@@ -673,7 +681,7 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd
             const int n = SBC * h + SBC * WPS * sbi + 64 * k + lane;
             xv[sbi][k] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
         }
-    const bool frozen = *su.err != 0;  // a bounds error this step: no table row is written
+    const bool frozen = su.single ? *su.err != 0 : true;  // a bounds error this step: no table row is written
     if (tdl_ok) {
         tds[threadIdx.x] = tdl;
         if constexpr (MAPPED) {
@@ -701,8 +709,9 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : 4) void interact_bwd
         const int kk = 4 * s + q;
         const uint32_t r = (uint32_t)__shfl((int)myrow, kk >= 1 ? kk - 1 : 0, 64);
         const bool tab = s < ksteps && kk >= 1 && kk < F && r != ~0u;
-        const T* src = (s < ksteps && kk == 0) ? x + bb * x_ld
-                                               : (tab ? (const T*)tds[kk - 1].data + (int64_t)r * d : nullptr);
+        const T* src = YS ? ((s < ksteps && kk < F) ? x + bb * x_ld + (int64_t)kk * d : nullptr)
+                   : (s < ksteps && kk == 0) ? x + bb * x_ld
+                                             : (tab ? (const T*)tds[kk - 1].data + (int64_t)r * d : nullptr);
         livek |= src ? (1u << s) : 0u;
         // (CPL = 8: a masked row reads the zero row -- a 16-B aligned source whatever dout's layout)
         rowp[s] = src ? src : (CPL == 8 ? (const T*)g_zero_row : ob);
@@ -1062,6 +1071,32 @@ static int run_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const
                              : ((uintptr_t)t % (4 * esz) == 0 && (t_ld % 4) == 0);
     const bool aligned = d % 4 == 0 && t_ok && (uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && (dx_ld % 4) == 0 &&
                          (dt_ld % 4) == 0;
+    // a materialized ys with 33..96 features (pooled bags): the split kernel's load plan, one wave
+    // per 64-column super-block (the one-wave-per-sample bwd_body kernel spills at NB = 5 and ran
+    // the pooled backward at 145 us); bit-identical (the same MFMA sums).  DLRM_BWD_YS = 0: bwd_body.
+    static const bool ys_split = !getenv("DLRM_BWD_YS") || atoi(getenv("DLRM_BWD_YS")) != 0;
+    const int wps = d >= 256 ? 4 : (d >= 128 ? 2 : 1);
+    if (!GATHER && ys_split && aligned && NB >= 3 && NB <= 6 && d == 64 * wps) {
+        const StepUpdate su{nullptr, 0, 0.0f, ctx_error_word(ctx)};
+#define DLRM_YS(TY, N_, W_)                                                                                         \
+    hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 0, 1, W_, false, 4, true>), dim3((unsigned)B),            \
+                       dim3(64 * W_), 0, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga,           \
+                       (const TY*)t, t_ld, su)
+#define DLRM_YS_W(TY, N_) \
+    if (wps == 4) DLRM_YS(TY, N_, 4); else if (wps == 2) DLRM_YS(TY, N_, 2); else DLRM_YS(TY, N_, 1);
+#define DLRM_YS_NB(TY)                                                                            \
+    switch (NB) {                                                                                 \
+        case 3: DLRM_YS_W(TY, 3) break;                                                           \
+        case 4: DLRM_YS_W(TY, 4) break;                                                           \
+        case 5: DLRM_YS_W(TY, 5) break;                                                           \
+        default: DLRM_YS_W(TY, 6) break;                                                          \
+    }
+        if (dtype == DLRM_F32) { DLRM_YS_NB(float) } else { DLRM_YS_NB(uint16_t) }
+#undef DLRM_YS_NB
+#undef DLRM_YS_W
+#undef DLRM_YS
+        return ctx_hip(ctx, hipGetLastError(), "interact_bwd(ys, split) launch");
+    }
     if (aligned && NB >= 1 && NB <= 7) {  // NB = 8 would need > 64 KB of dynamic LDS
         if (dtype == DLRM_F32)
             dispatch_bwd<float, GATHER>(NB, s, cus, d, F, B, dout, dout_ld, t, t_ld, dx, dx_ld, dt, dt_ld, ga, x, x_ld);

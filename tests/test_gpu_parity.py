@@ -158,7 +158,8 @@ def test_lookup_empty_batch(pkg, gpu):
 
 # ------------------------------------------------------------------ interaction
 @pytest.mark.parametrize("d,F,B", [(16, 8, 128), (4, 4, 4), (128, 27, 300), (32, 17, 65), (64, 33, 20),
-                                   (16, 1, 5), (16, 2, 9), (8, 65, 7), (12, 5, 10), (128, 100, 3)])
+                                   (16, 1, 5), (16, 2, 9), (8, 65, 7), (12, 5, 10), (128, 100, 3),
+                                   (128, 50, 33), (256, 65, 19), (64, 96, 5), (256, 40, 7)])
 def test_interaction_fwd_bwd_vs_oracle(pkg, gpu, d, F, B):
     rng = np.random.default_rng(d * 1000 + F)
     x = rng.standard_normal((B, d)).astype(np.float32)
@@ -789,6 +790,33 @@ def test_fused_lookup_interaction_equals_two_operators(pkg, gpu, rows, D, B, L, 
     hp.check_bounds()
     assert torch.equal(hp.ys, ys)    # lookup output + fast_vcat: bit-identical
     assert torch.equal(hp.out, out)  # same MFMA order: bit-identical
+
+
+@pytest.mark.parametrize("T,D,B,dtype", [(40, 64, 37, torch.float32), (64, 256, 29, torch.float32),
+                                         (50, 128, 21, torch.float32), (64, 256, 17, torch.bfloat16),
+                                         (90, 64, 11, torch.float32)])
+def test_ys_backward_equals_gather_backward(pkg, gpu, T, D, B, dtype):
+    """33 <= F <= 96: dlrm_interact_bwd on a materialized ys (the split kernel's load plan, one wave
+    per 64-column super-block) gives the bits of the re-gathering backward (bwd_body), whose MFMA
+    sums it shares."""
+    rng = np.random.default_rng(T * 7 + D)
+    rows = [int(r) for r in rng.integers(2, 5000, T)]
+    tabs = dev_tables(rand_tables(rng, rows, D), gpu, dtype)
+    idx = pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).reshape(T, B, 1).to(torch.int32).to(gpu))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
+    ts = pkg.EmbeddingTableSet(tabs)
+    a = pkg.HotPath(ts, B, 1, index_base=0, fused=True, materialize_ys=True, deterministic=False)
+    g = pkg.HotPath(ts, B, 1, index_base=0, fused=True, materialize_ys=False, deterministic=False)
+    dout = (torch.randn((B, a.width), device=gpu) * 1e-2).to(dtype)
+    a.forward(x, idx)
+    g.forward(x, idx)
+    a.interact_bwd(dout)
+    g.interact_bwd(dout, x=x, idx=idx)
+    torch.cuda.synchronize()
+    a.check_bounds()
+    assert torch.equal(a.out, g.out)
+    assert torch.equal(a.dx, g.dx)
+    assert torch.equal(a.dt[:, D:], g.dt[:, D:])
 
 
 def test_fused_bounds_error(pkg, gpu):
