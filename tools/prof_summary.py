@@ -121,8 +121,15 @@ def finish(kernels, workload, head, out_path):
         if "MFMA_BUSY_CYCLES_avg" in v and v.get("GRBM_GUI_ACTIVE_avg"):
             v["mfma_busy"] = busy(v)
     stages = defaultdict(lambda: {"avg_us": 0.0, "kernels": []})
+    # a stage's launch = its kernels that run every step: a kernel with fewer than half the calls of
+    # the stage's most-called one ran only while priming / capturing (e.g. the step forward that
+    # builds the first batch's indexer, before the pipelined steps' gather-only forwards)
+    top = defaultdict(int)
+    for v in kernels.values():
+        if v["stage"] is not None:
+            top[v["stage"]] = max(top[v["stage"]], v["calls"])
     for k, v in kernels.items():
-        if v["stage"] is None:
+        if v["stage"] is None or v["calls"] * 2 < top[v["stage"]]:
             continue
         s = stages[v["stage"]]
         s["avg_us"] += v["avg_us"]
