@@ -620,6 +620,8 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
                                                            (int)sizeof(StepLds));
         (void)attr;
         const int NI = pa->T << pa->ix.vshift;
+        static const int shrink = getenv("DLRM_APPLY_SHRINK") ? atoi(getenv("DLRM_APPLY_SHRINK")) : 0;  // A/B knob
+        if (shrink) grid = grid > NI ? grid - NI : 1;
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
                            sizeof(StepLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
                            *pa);
