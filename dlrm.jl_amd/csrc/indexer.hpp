@@ -17,7 +17,10 @@ enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
 // workgroup: 8 lane groups x 16 rows in flight at D = 128) each, so a hot row's grad rows are read
 // by several CUs at once; a segment of several slices is combined by its last-arriving slice (sc1
 // partial rows + a counter; apply.hpp).
-constexpr int kHotSlice = 128;
+#ifndef DLRM_HOT_SLICE
+#define DLRM_HOT_SLICE 128
+#endif
+constexpr int kHotSlice = DLRM_HOT_SLICE;
 // A chunk's descriptor is two int4: {beg, end, row, pos0}, {pos1, pos2, pos3, pos4}: its first
 // kChunkInline positions (ascending; -1 past the end) travel with it, so the apply reads perm
 // only for longer chunks.  A hot slice's descriptor is one int4 {p0, p1, row, hot segment}.

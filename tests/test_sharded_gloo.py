@@ -110,16 +110,19 @@ def _worker(rank, world, port, cfg, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,T,L,owners,micro", [
-    (2, 5, 1, None, 1), (2, 7, 3, None, 1), (3, 4, 1, None, 1), (3, 2, 2, None, 1),
-    (2, 5, 1, [[4, 0, 2], [1, 3]], 1), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 1),
-    (2, 5, 1, None, 2), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 2), (2, 7, 1, None, 4)])
-def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners, micro):
+@pytest.mark.parametrize("world,T,L,owners,micro,G", [
+    (2, 5, 1, None, 1, 0), (2, 7, 3, None, 1, 0), (3, 4, 1, None, 1, 0), (3, 2, 2, None, 1, 0),
+    (2, 5, 1, [[4, 0, 2], [1, 3]], 1, 0), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 1, 0),
+    (2, 5, 1, None, 2, 0), (3, 6, 2, [[5], [0, 2, 3, 4], [1]], 2, 0), (2, 7, 1, None, 4, 0),
+    # strong scaling (bench.py --global-batch): one global batch of 12 over 2 and 3 ranks
+    (2, 5, 1, None, 1, 12), (3, 5, 1, None, 1, 12), (3, 5, 1, None, 2, 12), (2, 6, 2, None, 3, 12)])
+def test_sharded_step_equals_single_process(tmp_path, pkg, world, T, L, owners, micro, G):
     """owners: explicit (non-contiguous) table assignment, as TablePartition.fitting makes.
-    micro: micro-batches per step (rank r's local sample b is global sample global_index(r, b))."""
+    micro: micro-batches per step (rank r's local sample b is global sample global_index(r, b)).
+    G: a fixed global batch split over the ranks (strong scaling); 0: 4 samples per rank (weak)."""
     import oracle
     rows = [3, 50, 1000, 7, 400, 12, 90][:T]
-    D, B, lr = 16, 4, 0.5
+    D, B, lr = 16, (G // world if G else 4), 0.5
     cfg = (T, rows, D, B, L, lr, owners, micro)
     mp.start_processes(_worker, args=(world, _free_port(), cfg, str(tmp_path)), nprocs=world, start_method="spawn")
     # single process on the global batch
