@@ -230,7 +230,7 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
     for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
         for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-    const int u1 = min(len, (gid + 1) * SPG);  // (SPG = kHotSlice / NG: one round of IF rows at D <= 128)
+    const int u1 = min(len, (gid + 1) * SPG);  // (SPG = kHotSlice / NG: two rounds of IF rows at D = 128)
     constexpr int IF = G::IF < SPG ? G::IF : SPG;
     for (int u0 = gid * SPG; u0 < u1; u0 += IF) {
         typename Vec<GT>::type gv[IF][G::VPL];

@@ -14,11 +14,14 @@ constexpr int kChunk = 32;          // max positions of a segment handled by one
 constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
 enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
 // Hot segments are cut into slices of kHotSlice positions, one work item (one 256-thread apply
-// workgroup: 8 lane groups x 16 rows in flight at D = 128) each, so a hot row's grad rows are read
+// workgroup: 8 lane groups x 16 rows in flight at D = 128, two rounds) each, so a hot row's grad rows are read
 // by several CUs at once; a segment of several slices is combined by its last-arriving slice (sc1
 // partial rows + a counter; apply.hpp).
+// 256 (round 3; was 128): fewer multi-slice segments to combine across workgroups.  A/B on one box
+// (tools/r6v_check.sh): bf16 B=8192 apply 22.4 -> 20.4 us (78.6 -> 80.2 M samples/s), D=16 +0.6 %,
+// pooled +0.4 %, the metric unchanged; 64 was slower everywhere.
 #ifndef DLRM_HOT_SLICE
-#define DLRM_HOT_SLICE 128
+#define DLRM_HOT_SLICE 256
 #endif
 constexpr int kHotSlice = DLRM_HOT_SLICE;
 // A chunk's descriptor is two int4: {beg, end, row, pos0}, {pos1, pos2, pos3, pos4}: its first
