@@ -229,16 +229,9 @@ __device__ __forceinline__ void fwd_body(int bid, int nblocks, float* stage_all,
     }
 }
 
-// Minimum waves per SIMD the compiler must fit: 4 for the bf16 one-hot kernels at NB <= 2 (four
-// sample waves resident per SIMD instead of three), else 2.
-#ifndef DLRM_FWD_BF16_WAVES
-#define DLRM_FWD_BF16_WAVES 4
-#endif
-template <typename T, int NB, bool POOL>
-constexpr int kFwdMinWaves = (sizeof(T) == 2 && NB <= 2 && !POOL) ? DLRM_FWD_BF16_WAVES : 2;
 // POOL: the pooled-bag path (lookups > 1) is compiled in; the one-hot kernel stays lean.
 template <typename T, int NB, bool FUSED, bool POOL, int DC = 0, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB, (kFwdMinWaves<T, NB, POOL>)) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
+__global__ __launch_bounds__(64 * WPB, 2) void interact_fwd_kernel(int d, int F, int B, const T* __restrict__ x,
                                                                    int64_t x_ld, T* __restrict__ ys, int64_t ys_ld,
                                                                    T* __restrict__ out, int64_t out_ld, int padding,
                                                                    GatherArgs ga, TabPtrs tp) {
