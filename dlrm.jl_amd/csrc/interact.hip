@@ -841,9 +841,15 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : (NB > 2 ? 2 : 4)) vo
                         for (int e = 0; e < CPL; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
                         store_row<T, CPL, true>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
                     } else if constexpr (!mapped) {
+                        // (CPL = 8: a lane's two 16-B pieces are 32 B apart, so each store instruction
+                        // covers half of every line: plain stores let L2 merge the halves, where
+                        // non-temporal ones left as partial-line writes, 95 -> 117 MB per launch)
 #pragma unroll
-                        for (int e = 0; e < CPL; e += 4)
-                            stg_nt<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0 + e, f32x4_t{v[e], v[e + 1], v[e + 2], v[e + 3]});
+                        for (int e = 0; e < CPL; e += 4) {
+                            const f32x4_t pv4 = f32x4_t{v[e], v[e + 1], v[e + 2], v[e + 3]};
+                            if constexpr (CPL == 8) stg<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0 + e, pv4);
+                            else stg_nt<f32x4_t>(dt + b * dt_ld + (int64_t)f * d + n0 + e, pv4);
+                        }
                     } else if (f > 0) {
 #pragma unroll
                         for (int e = 0; e < CPL; e += 4)
