@@ -393,6 +393,108 @@ double run2(Tabs tabs, const int* idx, const float* x, float* out, const float* 
     return ms * 1e3 / reps;
 }
 
+// Software-pipelined forward: SPW samples per wave, every index load of all SPW samples, then
+// every row load (sample 0's first), then per sample: MFMAs (even / odd parity partials, the
+// shipped order) + staging + stores.  Sample s's MFMAs wait only for its own loads, so they
+// run while the later samples' rows are still arriving; only the last sample's tail is exposed.
+template <int SPW, int WPB, int OCC>
+__global__ __launch_bounds__(64 * WPB, OCC) void fwdp(Tabs tabs, const int* __restrict__ idx, const float* __restrict__ x,
+                                                     float* __restrict__ out, const float* __restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) float stage_all[WPB][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 15, q = lane >> 4;
+    const int b0 = (blockIdx.x * WPB + w) * SPW;
+    float* stage = stage_all[w];
+    int ri[SPW][2];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int I = 0; I < 2; ++I) {
+            const int row = I * 16 + c;
+            ri[s][I] = (row >= 1 && row < F) ? idx[(row - 1) * B + b0 + s] : 0;
+        }
+    const float* src[SPW][2];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int I = 0; I < 2; ++I) {
+            const int row = I * 16 + c;
+            src[s][I] = row == 0 ? x + (size_t)(b0 + s) * D : (row < F ? tabs.p[row - 1] + (size_t)ri[s][I] * D : zero);
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    f4 a[SPW][8][2];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int uu = 0; uu < 8; ++uu)
+#pragma unroll
+            for (int I = 0; I < 2; ++I) a[s][uu][I] = *(const f4*)(src[s][I] + uu * 16 + q * 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+        f4 acc[2][3];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc[p][k] = f4{0, 0, 0, 0};
+#pragma unroll
+        for (int uu = 0; uu < 8; ++uu) {
+            int ij = 0;
+#pragma unroll
+            for (int I = 0; I < 2; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J, ++ij)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        acc[uu & 1][ij] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][uu][I][k], a[s][uu][J][k], acc[uu & 1][ij], 0, 0, 0);
+        }
+        if (c == 0)
+#pragma unroll
+            for (int uu = 0; uu < 8; ++uu) *(f4*)(stage + uu * 16 + q * 4) = a[s][uu][0];
+        int ij = 0;
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J, ++ij) {
+                const f4 z = acc[0][ij] + acc[1][ij];
+                const int j = J * 16 + c;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = I * 16 + 4 * q + r;
+                    if (i < F && j < i) stage[D + i * (i - 1) / 2 + j] = z[r];
+                }
+            }
+        if (lane == 0) stage[W - 1] = 0.f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float* orow = out + (size_t)(b0 + s) * W;
+        for (int e = lane; e < W; e += 64) orow[e] = stage[e];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int SPW, int WPB, int OCC>
+double runp(Tabs tabs, const int* idx, const float* x, float* out, const float* zero) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const int grid = B / (WPB * SPW);
+    for (int i = 0; i < NBATCH; ++i)
+        hipLaunchKernelGGL((fwdp<SPW, WPB, OCC>), dim3(grid), dim3(64 * WPB), 0, 0, tabs, idx + (size_t)i * T * B, x, out, zero);
+    const int reps = 4 * NBATCH;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((fwdp<SPW, WPB, OCC>), dim3(grid), dim3(64 * WPB), 0, 0, tabs, idx + (size_t)(i % NBATCH) * T * B,
+                           x, out, zero);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e3 / reps;
+}
+
 int main() {
     static const int64_t kaggle[T] = {1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194,
                                       27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572};
@@ -464,6 +566,13 @@ int main() {
             CK(hipFree(zf));
             CK(hipFree(dtabs)); CK(hipFree(err));
         }
+        printf("%s pipelined spw1 wpb4   %7.2f us\n", lname, runp<1, 4, 2>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw2 wpb4   %7.2f us\n", lname, runp<2, 4, 1>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw2 wpb4 o2%7.2f us\n", lname, runp<2, 4, 2>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw2 wpb2   %7.2f us\n", lname, runp<2, 2, 2>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw2 wpb1   %7.2f us\n", lname, runp<2, 1, 2>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw4 wpb2   %7.2f us\n", lname, runp<4, 2, 1>(tabs, idx, x, out, zero));
+        printf("%s pipelined spw4 wpb1   %7.2f us\n", lname, runp<4, 1, 1>(tabs, idx, x, out, zero));
         printf("%s empty           wpb4 %7.2f us\n", lname, run<8, 4>(tabs, idx, x, out, zero));
         printf("%s index only      wpb4 %7.2f us\n", lname, run<4, 4>(tabs, idx, x, out, zero));
         printf("%s gather+mfma+out wpb4 %7.2f us\n", lname, run<3, 4>(tabs, idx, x, out, zero));
