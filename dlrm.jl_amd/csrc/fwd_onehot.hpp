@@ -97,6 +97,25 @@ struct GatherArgs {
 // (wave h takes the steps of parity h: half the loads and MFMAs per wave, twice the waves in
 // flight; tools/fwd_probe.hip: 10.2 vs 11.5 us at the metric shape), the odd wave's tiles handed
 // to the even wave through LDS.
+// The staged output row written 4 elements per lane (16-B fp32 stores: a quarter of the store
+// instructions of one element per lane); DLRM_FWD_VEC_OUT=0 keeps the scalar stores.
+#ifndef DLRM_FWD_VEC_OUT
+#define DLRM_FWD_VEC_OUT 1
+#endif
+constexpr bool kFwdVecOut = DLRM_FWD_VEC_OUT;
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const f32x4_t& v) {
+    if constexpr (sizeof(T) == 4) {
+        stg<f32x4_t>((f32x4_t*)p, v);
+    } else {
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        u32x2_t u;
+        u[0] = (uint32_t)from_f32<T>(v[0]) | ((uint32_t)from_f32<T>(v[1]) << 16);
+        u[1] = (uint32_t)from_f32<T>(v[2]) | ((uint32_t)from_f32<T>(v[3]) << 16);
+        stg<u32x2_t>((u32x2_t*)p, u);
+    }
+}
+
 template <typename T, int NB> struct FwdPart {
     static constexpr int NT = NB * (NB + 1) / 2;  // lower-triangle tiles
 };
@@ -130,6 +149,10 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
     f32x4_t* xch = (f32x4_t*)(stage_all + SPB * kStage) + pair * NT * 64;
     const T* zero = (const T*)g_zero_row;
     constexpr int ZMASK = kZeroElems * 4 / (int)sizeof(T) - 1;
+    // the staged output row leaves as 16-B stores when every row start is aligned for them (fp32 at
+    // d = 128: forward 12.1 -> 11.4 us, r8d; at d = 16 and for bf16 rows no gain: scalar stores)
+    constexpr bool VEC_OUT = kFwdVecOut && sizeof(T) == 4 && DC >= 128;
+    const bool vec_out = W % 4 == 0 && out_ld % 4 == 0 && ((uintptr_t)out & (4 * sizeof(T) - 1)) == 0;
     bool bad_any = false;  // an out-of-range index was skipped (zero row) by this lane
     for (int64_t b0 = (int64_t)bid * SPB; b0 < B; b0 += (int64_t)nblocks * SPB) {
         const int64_t bs = b0 + pair;
@@ -284,7 +307,9 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
         }
         if (staged) {
             if constexpr (WPS == 1) wave_lds_sync(); else __syncthreads();
-            if (live)
+            if (live && VEC_OUT && vec_out)
+                for (int e = 4 * (lane + 64 * h); e < W; e += 256 * WPS) store4<T>(orow + e, *(const f32x4_t*)(stage + e));
+            else if (live)
                 for (int e = lane + 64 * h; e < W; e += 64 * WPS) stg<T>(orow + e, from_f32<T>(stage[e]));
             if constexpr (WPS == 1) wave_lds_sync(); else __syncthreads();
         } else if constexpr (WPS == 2) {
