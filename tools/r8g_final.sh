@@ -11,3 +11,9 @@ for m in 1 2; do
   timeout -k 10 150 python tools/shard_sim.py --micro $m > $O/shard_sim_w8_m$m.json 2> $O/shard_sim_w8_m$m.err || { tail $O/shard_sim_w8_m$m.err; exit 1; }
   cat $O/shard_sim_w8_m$m.json
 done
+# A/B: non-temporal 16-B forward output stores (exp/ntout)
+for v in "" _ntout; do
+  lib=""; [ -n "$v" ] && lib=exp/ntout/libdlrm_hip.so
+  env ${lib:+DLRM_HIP_LIB=$lib} timeout -k 10 300 python bench.py --no-cpu-baseline --chain 0 > $O/ab$v.json 2> $O/ab$v.err || { tail $O/ab$v.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/ab$v.json'));print('ab$v',round(d['value']/1e6,3),d['ms_per_step'],{k:v['us'] for k,v in d['roofline']['stages'].items()})"
+done
