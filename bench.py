@@ -407,7 +407,7 @@ def main():
     # i.e. the fused step kernels reached through the reference's operator API (dlrm.jl_amd/lazy.py)
     chain = None
     if world == 1 and L == 1 and a.chain and graphs is not None:
-        ht = pkg.HipTables(ts, lr=a.lr)
+        ht = pkg.HipTables(ts, lr=a.lr, index_base=0)
         dot = pkg.DotInteraction()
         strat = pkg.PreallocationStrategy(D)
 

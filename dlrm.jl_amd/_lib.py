@@ -21,6 +21,7 @@ F32, BF16 = 0, 1
 I32, I64 = 0, 1
 UPDATE_ATOMIC, UPDATE_PREBUILT = 1, 2
 STEP_BWD_ONLY, STEP_APPLY_ONLY = 1, 2
+IX_BUILT, IX_SPLIT, IX_PREPARED, IX_SINGLES_DONE = 1, 2, 4, 8
 COMM_ID_BYTES = 128
 
 
@@ -80,6 +81,7 @@ SIGNATURES = {
     "dlrm_indexer_destroy": (_i32, [_vp]),
     "dlrm_indexer_build": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32]),
     "dlrm_indexer_read": (_i32, [_vp, _vp, _i32, _pi64, _pi64, _pi64, _pi64, _i64]),
+    "dlrm_indexer_state": (_i32, [_vp, ctypes.POINTER(ctypes.c_uint)]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
     "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),

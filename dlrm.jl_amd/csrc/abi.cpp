@@ -59,6 +59,17 @@ namespace dlrm {
 unsigned* ctx_error_word(dlrm_ctx* ctx) { return ctx->err; }
 hipStream_t ctx_stream(dlrm_ctx* ctx) { return ctx->stream; }
 int ctx_num_cus(dlrm_ctx* ctx) { return ctx->cus; }
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+const Knobs& knobs() {
+    static const Knobs k{env_int("DLRM_STEP_PARTS", 0),       env_int("DLRM_BUILD_PARTS", 0),
+                         env_int("DLRM_RELU_2PASS", 1) == 0, env_int("DLRM_BWD_YS", 1) == 0,
+                         env_int("DLRM_BWD_SPLIT", 1) == 0,  env_int("DLRM_BWD_SPB", 0),
+                         env_int("DLRM_BWD_CPL", 0),         env_int("DLRM_UPD_SBU", 1)};
+    return k;
+}
 int ctx_device(dlrm_ctx* ctx) { return ctx->device; }
 int ctx_fail(dlrm_ctx* ctx, int code, const char* fmt, ...) {
     if (ctx) {
@@ -87,7 +98,7 @@ static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device
 // workgroups than they save in sort depth beside the D = 128 gather); inside the apply launch
 // for rows of <= 256 B 8 parts (D = 16: apply + build 12.8 -> 11.4 us), for fp32 x 128 4.
 static int step_parts_log2(int dflt = kStepParts) {
-    static const int forced = getenv("DLRM_STEP_PARTS") ? atoi(getenv("DLRM_STEP_PARTS")) : 0;
+    const int forced = knobs().step_parts;
     const int p = forced > 0 ? forced : dflt;
     return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
 }
@@ -595,11 +606,8 @@ int dlrm_indexer_destroy(dlrm_indexer* ix) {
 
 // vshift of a standalone split build of N positions per table: the parts build where it applies
 static int build_vshift(const dlrm_indexer* ix, int64_t N, bool split) {
-    static const int lg = [] {  // DLRM_BUILD_PARTS = 2, 4 or 8 overrides (comparison runs)
-        const char* e = getenv("DLRM_BUILD_PARTS");
-        const int p = e ? atoi(e) : (1 << kPartsLog2);
-        return p >= 8 ? 3 : (p >= 4 ? 2 : 1);
-    }();
+    const int p = knobs().build_parts ? knobs().build_parts : (1 << kPartsLog2);
+    const int lg = p >= 8 ? 3 : (p >= 4 ? 2 : 1);
     return split && N > kFastMaxN && N <= kPartsMaxN && ix->TV == kStepMaxParts * ix->T ? lg : 0;
 }
 
@@ -661,6 +669,13 @@ static int read_indexer_table(dlrm_ctx* ctx, const dlrm_indexer* ix, int v, Inde
         rc = ctx_hip(ctx, hipMemcpy(o.seg_start.data(), ix->dev.seg_start + (int64_t)v * (ix->dev.cap + 1),
                                     (U + 1) * 4, hipMemcpyDeviceToHost), "read");
     return rc;
+}
+
+int dlrm_indexer_state(const dlrm_indexer* ix, unsigned* state) {
+    if (!ix || !state) return DLRM_E_ARG;
+    *state = (ix->built ? DLRM_IX_BUILT : 0u) | (ix->split ? DLRM_IX_SPLIT : 0u) |
+             (ix->prepared ? DLRM_IX_PREPARED : 0u) | (ix->singles_done ? DLRM_IX_SINGLES_DONE : 0u);
+    return DLRM_OK;
 }
 
 int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t* num_unique, int64_t* rows,
@@ -860,8 +875,16 @@ static int step_bwd_impl(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, const
     // gather backward writes every dt row and the apply takes a split indexer's once-hit rows too
     const bool split_bwd = ix->split && step_split_supported(tb->aligned16, tb->T, tb->dtype, d, x, x_ld);
     if (flags & DLRM_STEP_APPLY_ONLY) {
+        // the apply of a split build only completes a backward that stepped the once-hit rows
+        if (split_bwd && !ix->singles_done)
+            return ctx_fail(ctx, DLRM_E_STATE, "dlrm_step_bwd(APPLY_ONLY): no backward has run on this build");
         rc = DLRM_OK;
     } else if (split_bwd) {
+        // a second backward on one build would step its once-hit rows twice
+        if (ix->singles_done)
+            return ctx_fail(ctx, DLRM_E_STATE,
+                            "dlrm_step_bwd: this build's once-hit rows were already stepped (one backward per "
+                            "dlrm_step_fwd)");
         CHECK_ARG((uintptr_t)dx % 16 == 0 && (uintptr_t)dt % 16 == 0 && dx_ld % 4 == 0 && dt_ld % 4 == 0,
                   "dlrm_step_bwd: dx and dt must be 16-B aligned with leading dimensions divisible by 4");
         rc = launch_step_bwd(ctx, tb->d_desc, tb->T, tb->dtype, indices, itype, table_stride, index_base, d, batch, x,

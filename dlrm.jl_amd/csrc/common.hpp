@@ -256,6 +256,21 @@ int ctx_hip(dlrm_ctx* ctx, hipError_t e, const char* what);
 int ctx_num_cus(dlrm_ctx* ctx);
 int ctx_device(dlrm_ctx* ctx);
 
+// Comparison knobs: every environment variable the library reads, read once (abi.cpp), in this
+// one place.  0 = the default (the measured-best form); a non-zero value forces a variant for
+// A/B runs.  None is needed for correctness.
+struct Knobs {
+    int step_parts;   // DLRM_STEP_PARTS  (1/2/4/8): table parts of the step's split indexer build
+    int build_parts;  // DLRM_BUILD_PARTS (2/4/8): parts of a standalone split build, 4096 < N <= 8192
+    int relu_1pass;   // DLRM_RELU_2PASS=0: the one-launch (last-arriver) relu seam instead of two launches
+    int bwd_ys_body;  // DLRM_BWD_YS=0: the bwd_body kernel for a materialized ys with 33..96 features
+    int bwd_nosplit;  // DLRM_BWD_SPLIT=0: the one-wave step backward instead of the split kernel
+    int bwd_spb;      // DLRM_BWD_SPB (2/4/8): samples per block of the split step backward
+    int bwd_cpl;      // DLRM_BWD_CPL (4/8): columns per lane of the bf16 split step backward
+    int upd_sbu;      // DLRM_UPD_SBU (1/2): super-blocks in flight in the one-wave step backward
+};
+const Knobs& knobs();
+
 int launch_maplookup(dlrm_ctx* ctx, const TableDesc* d_tabs, bool tabs_aligned16, int T, int D, int dtype,
                      const void* idx, int itype, int64_t tstride, int base, int B, int L, void* out,
                      int64_t out_ld, int64_t out_off, const TableDesc* htabs = nullptr);

@@ -256,7 +256,7 @@ int launch_relu_bwd_bias(dlrm_ctx* ctx, int B, int N, const float* y, int64_t y_
     const dim3 grid((unsigned)relu_bwd_groups(N), (unsigned)relu_bwd_chunks(B));
     // default: the two-launch form (full step 483 vs 504-509 us with the last-arriver form on MI355X);
     // DLRM_RELU_2PASS=0 selects the one-launch last-arriver form
-    static const bool two_pass = !(getenv("DLRM_RELU_2PASS") && atoi(getenv("DLRM_RELU_2PASS")) == 0);
+    const bool two_pass = !knobs().relu_1pass;
     if (two_pass) {
         hipLaunchKernelGGL(relu_mask_partial_kernel, grid, dim3(kReluThreads), 0, ctx_stream(ctx), B, N, y, y_ld, g,
                            g_ld, part);

@@ -235,6 +235,7 @@ __device__ void fast_index_table(const IndexerDev& ix, int v, int t, int vs, uin
                                  unsigned* __restrict__ err, FastLds<NT, EPL, DB>& sl) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int S = 64 * EPL;
+    PHASE(0);
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
     const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
     const int nbits = 32 - __clz(kmax);

@@ -1080,7 +1080,7 @@ static int run_interact_bwd(dlrm_ctx* ctx, int dtype, int d, int F, int B, const
     // a materialized ys with 33..96 features (pooled bags): the split kernel's load plan, one wave
     // per 64-column super-block (the one-wave-per-sample bwd_body kernel spills at NB = 5 and ran
     // the pooled backward at 145 us); bit-identical (the same MFMA sums).  DLRM_BWD_YS = 0: bwd_body.
-    static const bool ys_split = !getenv("DLRM_BWD_YS") || atoi(getenv("DLRM_BWD_YS")) != 0;
+    const bool ys_split = !knobs().bwd_ys_body;
     const int wps = d >= 256 ? 4 : (d >= 128 ? 2 : 1);
     if (!GATHER && ys_split && aligned && NB >= 3 && NB <= 6 && d == 64 * wps) {
         const StepUpdate su{nullptr, 0, 0.0f, ctx_error_word(ctx)};
@@ -1275,16 +1275,12 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
     StepUpdate su{ix.single, ix.cap, lr, ctx_error_word(ctx)};
     // one super-block of T rows in flight: two (the gather backward's choice) spill here
-    static const int sbu = getenv("DLRM_UPD_SBU") ? atoi(getenv("DLRM_UPD_SBU")) : 1;  // experiment knob
+    const int sbu = knobs().upd_sbu;
     // d = 128 (two 64-column super-blocks): two waves per sample (interact_bwd_split_kernel)
-    static const bool split = !getenv("DLRM_BWD_SPLIT") || atoi(getenv("DLRM_BWD_SPLIT")) != 0;
+    const bool split = !knobs().bwd_nosplit;
     if (split && d == 128) {
         // samples per block (DLRM_BWD_SPB = 2, 4 or 8 overrides)
-        static const int spb_env = [] {
-            const char* e = getenv("DLRM_BWD_SPB");
-            const int v = e ? atoi(e) : 0;
-            return v >= 8 ? 8 : (v >= 4 ? 4 : (v > 0 ? 2 : 0));
-        }();
+        const int spb_env = knobs().bwd_spb >= 8 ? 8 : (knobs().bwd_spb >= 4 ? 4 : (knobs().bwd_spb > 0 ? 2 : 0));
 #define DLRM_LAUNCH_SPLIT(TY, N_, S_)                                                                              \
     hipLaunchKernelGGL((interact_bwd_split_kernel<TY, N_, 128, S_>), dim3((unsigned)((B + S_ - 1) / S_)),            \
                        dim3(128 * S_), 0, s, d, F, B, (const TY*)dout, dout_ld, dx, dx_ld, dt, dt_ld, ga, (const TY*)x,  \
@@ -1297,7 +1293,7 @@ int launch_step_bwd(dlrm_ctx* ctx, const TableDesc* tabs, int T_, int dtype, con
         // (kaggle-d128-b8192-bf16: backward 52.2 -> 48.4 us, step 110.9 -> 103.3 us, r6q; at B = 2048
         // the two-wave form keeps the step shorter: Terabyte rows 50.6 vs 48.7 M samples/s, r6s).
         // DLRM_BWD_CPL = 4 / 8 forces either form.
-        static const int cpl_env = getenv("DLRM_BWD_CPL") ? atoi(getenv("DLRM_BWD_CPL")) : 0;
+        const int cpl_env = knobs().bwd_cpl;
         const bool cpl8 = dtype != DLRM_F32 && (cpl_env ? cpl_env == 8 : B > 2048);
         const int spb = spb_env ? spb_env : (cpl8 ? 2 : 4);
 #define DLRM_LAUNCH_SPLIT8(N_, S_)                                                                                 \

@@ -50,14 +50,15 @@ __global__ __launch_bounds__(256) void maplookup_vec(const TableDesc* __restrict
     const vt* zero = (const vt*)g_zero_row;
     bool bad = false;
 
-    for (int first = wave * (RPW * U); first < total; first += nwaves * (RPW * U)) {
+    // (64-bit cursor: total < 2^31, but total + a grid stride need not be)
+    for (int64_t first = (int64_t)wave * (RPW * U); first < total; first += (int64_t)nwaves * (RPW * U)) {
         int bb[U], tt[U];
         bool live[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int item = first + u * RPW + g;
+            const int64_t item = first + u * RPW + g;
             live[u] = item < total;
-            const int it = live[u] ? item : 0;
+            const int it = live[u] ? (int)item : 0;
             bb[u] = it / ntab;
             tt[u] = it - bb[u] * ntab;
         }

@@ -23,8 +23,6 @@
 // bitwise reproducible, and no inter-workgroup hand-off.  DLRM_UPDATE_ATOMIC instead adds
 // -lr*g straight into the table with global_atomic_add_f32 (no sort, non-deterministic
 // rounding order).
-#include <cstdlib>
-
 #include "common.hpp"
 
 #ifdef DLRM_PHASE
@@ -32,7 +30,12 @@
 // built only into the profiling variant of the library (tools/phase_indexer.py).
 __device__ unsigned long long g_phase[64];
 __device__ unsigned long long g_blk[2][256];
-#define PHASE(k) do { __syncthreads(); if (blockIdx.x == DLRM_PHASE && threadIdx.x == 0) g_phase[k] = wall_clock64(); } while (0)
+__device__ unsigned long long g_phase2[256][32];  // every block < 256: marks k < 32
+#define PHASE(k) do { __syncthreads(); if (threadIdx.x == 0) { const unsigned long long c_ = wall_clock64(); \
+    if (blockIdx.x == DLRM_PHASE) g_phase[k] = c_; if (blockIdx.x < 256 && (k) < 32) g_phase2[blockIdx.x][k] = c_; } } while (0)
+extern "C" int dlrm_debug_phase2(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase2), sizeof(g_phase2));
+}
 __device__ unsigned long long g_apply[3][32768];  // start, end, kind of every apply block
 #define APPLY_START(kind) do { if (threadIdx.x == 0) { const int blk_ = blockIdx.y * gridDim.x + blockIdx.x; \
     if (blk_ < 32768) { g_apply[0][blk_] = wall_clock64(); g_apply[2][blk_] = (kind); } } } while (0)
@@ -50,7 +53,22 @@ extern "C" int dlrm_debug_apply_reset(void) {
     static unsigned long long z[3][32768];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_apply), z, sizeof(z));
 }
+// per-item log of the apply launch: slot = block * 16 + k (its k-th item): start, end, kind | item << 8
+__device__ unsigned long long g_item[3][65536];
+#define ITEM_START(kind, k, item) do { const int s_ = (blockIdx.x * 16 + (k)); if (threadIdx.x == 0 && (k) < 16 && s_ < 65536) { \
+    g_item[0][s_] = wall_clock64(); g_item[2][s_] = (unsigned long long)(kind) | ((unsigned long long)(item) << 8); } } while (0)
+#define ITEM_END(k) do { const int s_ = (blockIdx.x * 16 + (k)); if ((threadIdx.x & 63) == 0 && (k) < 16 && s_ < 65536) \
+    atomicMax(&g_item[1][s_], wall_clock64()); } while (0)
+extern "C" int dlrm_debug_items(unsigned long long* out, int reset) {
+    if (reset) {
+        static unsigned long long z[3][65536];
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_item), z, sizeof(z));
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_item), sizeof(g_item));
+}
 #else
+#define ITEM_START(kind, k, item) do {} while (0)
+#define ITEM_END(k) do {} while (0)
 #define PHASE(k) do {} while (0)
 #define APPLY_START(kind) do {} while (0)
 #define APPLY_END() do {} while (0)
@@ -346,9 +364,11 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
         const int NI = pa.T << pa.ix.vshift;
         if (bid < NI) {
             const int vv = bid, t = vv >> pa.ix.vshift;
+            ITEM_START(4, 0, vv);
             fast_index_table<256, kStepIndexEPL, true>(pa.ix, vv, t, pa.ix.vshift, (uint32_t)load_table(pa.tabs, t).nrows,
                                                        pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
                                                        *(StepLds*)prep_lds);
+            ITEM_END(0);
             return;
         }
         bid -= NI;
@@ -391,9 +411,18 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
         pos0 = bid >> 3;
         step = nblk >> 3;
     }
+#ifdef DLRM_PHASE
+    int kk_ = 0;
+#endif
     for (int pos = pos0; pos < npos; pos += step) {
         const int item = pos + (pos < e0 ? r0 : (pos < e1 ? s1 : s2));
         APPLY_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2));
+#ifdef DLRM_PHASE
+        const int k_ = kk_++;
+        ITEM_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2), k_, item);
+#undef APPLY_END
+#define APPLY_END() do { ITEM_END(k_); } while (0)
+#endif
         if (SG && item >= citems) {  // uniform: once-hit positions of one real table
             const int t = (item - citems) / per_t;
             const int p0 = ((item - citems) - t * per_t) * SP + gid * G::SPPG;
@@ -424,6 +453,10 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
                                sm);
         APPLY_END();
     }
+#ifdef DLRM_PHASE
+#undef APPLY_END
+#define APPLY_END() do {} while (0)
+#endif
 }
 
 // The step indexer's workgroups alone (PrepArgs), where the apply has no vector kernel to host them.
@@ -565,13 +598,10 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     hipStream_t s = stream ? stream : ctx_stream(ctx);
     const int64_t N = (int64_t)B * L;
     unsigned* err = ctx_error_word(ctx);
-    static const bool ix256 = getenv("DLRM_IX256") != nullptr;  // experiment knob
     if (ix.vshift > 0) {  // the caller chose the parts build (kFastMaxN < N <= kPartsMaxN, split)
         if (!split || N > kPartsMaxN)
             return ctx_fail(ctx, DLRM_E_ARG, "indexer parts build: N=%lld split=%d", (long long)N, (int)split);
         launch_fast<1024, 8, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
-    } else if (ix256 && N <= 2048 && !split) {  // the 256-thread form the forward / backward launches use, on its own
-        launch_fast<256, 8, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
     } else if (N <= 1024 * 2) {
         if (split) launch_fast<1024, 2, true>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
         else launch_fast<1024, 2, false>(s, ix, tabs, T_, idx, itype, tstride, base, (int)N, err);
@@ -620,8 +650,6 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
                                                            (int)sizeof(StepLds));
         (void)attr;
         const int NI = pa->T << pa->ix.vshift;
-        static const int shrink = getenv("DLRM_APPLY_SHRINK") ? atoi(getenv("DLRM_APPLY_SHRINK")) : 0;  // A/B knob
-        if (shrink) grid = grid > NI ? grid - NI : 1;
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
                            sizeof(StepLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
                            *pa);

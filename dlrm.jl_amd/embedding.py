@@ -180,17 +180,24 @@ class PackedIndices:
         return itype_code(self.data.dtype)
 
 
-def maplookup(strategy, tables, sparse, *, index_base=1, out=None, check_bounds=True):
+def maplookup(strategy, tables, sparse, *, index_base=None, out=None, check_bounds=True):
     """maplookup(strategy, tables, sparse) (EmbeddingTables; model.jl:161).
 
     PreallocationStrategy(P): returns [B][P + D*T]; row b holds [<untouched P> | e_1 | ... | e_T]
     where e_t = sum_k table_t[idx_t[b, k]] (sum pooling for multi-hot bags).
     DefaultStrategy(): returns a list of per-table [B][D] tensors.
     Raises BoundsError on an out-of-range index when check_bounds (synchronises).
-    With `HipTables` (lazy.py): a LazyLookup, gathered by the interaction's fused kernel."""
+    index_base: 1 (Julia) unless given.
+    With `HipTables` (lazy.py): a LazyLookup, gathered by the interaction's fused kernel; the
+    tables carry the index base (a different `index_base` raises) and `out` is not taken."""
     from .lazy import HipTables, maplookup_lazy
     if isinstance(tables, HipTables):
-        return maplookup_lazy(strategy, tables, sparse)
+        tables.check_index_base(index_base, "maplookup")
+        if out is not None:
+            raise ValueError("maplookup on HipTables defers the gather into the interaction: no `out` buffer "
+                             "(materialize the LazyLookup, or pass the plain table set)")
+        return maplookup_lazy(strategy, tables, sparse, check_bounds=check_bounds)
+    index_base = 1 if index_base is None else int(index_base)
     ts = as_table_set(tables)
     idx = PackedIndices(sparse, device=ts.device)
     require_device(idx.data, ts.device, "indices")

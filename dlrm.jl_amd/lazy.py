@@ -36,11 +36,17 @@ class HipTables:
     interaction.  lr: the Descent η the following update! will use (lets the backward apply the
     once-hit rows itself, the fastest form); None: update! applies every row."""
 
-    def __init__(self, tables, *, lr=None, index_base=0):
+    def __init__(self, tables, *, lr=None, index_base=1):
         self.ts = as_table_set(tables) if not isinstance(tables, EmbeddingTableSet) else tables
         self.lr = None if lr is None else float(lr)
-        self.index_base = int(index_base)
+        self.index_base = int(index_base)  # 1: Julia's, as maplookup / update_ default to
         self._hp = {}
+
+    def check_index_base(self, index_base, op):
+        """A caller-passed index base must be the tables' own (None: the tables')."""
+        if index_base is not None and int(index_base) != self.index_base:
+            raise ValueError(f"{op}: index_base={index_base}, but these HipTables were built with "
+                             f"index_base={self.index_base}")
 
     def __len__(self):
         return len(self.ts)
@@ -70,8 +76,9 @@ class HipTables:
 class LazyLookup:
     """maplookup(PreallocationStrategy(P), ::HipTables, sparse) before anything is gathered."""
 
-    def __init__(self, tables, idx, prealloc):
+    def __init__(self, tables, idx, prealloc, check_bounds=True):
         self.tables, self.idx, self.prealloc = tables, idx, int(prealloc)
+        self.check_bounds = bool(check_bounds)  # materialize()'s default
 
     @property
     def shape(self):
@@ -85,11 +92,12 @@ class LazyLookup:
     def device(self):
         return self.tables.ts.device
 
-    def materialize(self, check_bounds=True):
+    def materialize(self, check_bounds=None):
         """The ys the reference's maplookup returns (one dlrm_maplookup launch)."""
         from .embedding import maplookup
+        cb = self.check_bounds if check_bounds is None else check_bounds
         return maplookup(PreallocationStrategy(self.prealloc), self.tables.ts, self.idx,
-                         index_base=self.tables.index_base, check_bounds=check_bounds)
+                         index_base=self.tables.index_base, check_bounds=cb)
 
     # -- the interaction on it: dlrm_step_fwd
     def interact(self, x):
@@ -129,15 +137,17 @@ class DeferredUpdate(SparseEmbeddingUpdate):
         return super().uncompress(nrows, index_base=index_base)
 
 
-def maplookup_lazy(strategy, tables, sparse):
+def maplookup_lazy(strategy, tables, sparse, check_bounds=True):
+    """(Bounds of a LazyLookup's indices are raised by the fused forward's flag: at update_ with
+    check_bounds, or at the next check_bounds.)"""
     idx = PackedIndices(sparse, device=tables.ts.device)
     if idx.T != len(tables):
         raise ValueError(f"{idx.T} index arrays for {len(tables)} tables")
     if isinstance(strategy, PreallocationStrategy) and idx.L == 1:
-        return LazyLookup(tables, idx, strategy.prealloc)
+        return LazyLookup(tables, idx, strategy.prealloc, check_bounds)
     # pooled bags / DefaultStrategy: the plain operator (no fused step form)
     from .embedding import maplookup
-    return maplookup(strategy, tables.ts, idx, index_base=tables.index_base)
+    return maplookup(strategy, tables.ts, idx, index_base=tables.index_base, check_bounds=check_bounds)
 
 
 def rrule_lazy(x, ys):
@@ -147,10 +157,13 @@ def rrule_lazy(x, ys):
 
     def dot_pullback(delta):
         if tables.lr is not None:  # once-hit rows stepped here (w = fmaf(-η, g, w)), the rest left in dt
+            # (a second pullback on this forward is refused by the library: it would step them twice)
             hp.step_bwd(delta, x=x, idx=idx, flags=_lib.STEP_BWD_ONLY)
         else:                      # every dt row written; update! steps every row
             hp.interact_bwd(delta, x=x, idx=idx)
-        return None, hp.dx, LazyGrad(hp, idx, x, delta, tables.lr is not None)
+        # applied: the split backward ran (a shape without it writes every dt row, as above)
+        applied = bool(hp.indexer.state() & _lib.IX_SINGLES_DONE)
+        return None, hp.dx, LazyGrad(hp, idx, x, delta, applied)
 
     return hp.out, dot_pullback
 

@@ -111,6 +111,12 @@ class SparseIndexer:
         self._built_from = idx
         return self
 
+    def state(self):
+        """Host-side state of the last build: a mask of _lib.IX_* bits (no GPU call)."""
+        st = ctypes.c_uint()
+        self.ctx.check(self.ctx.lib.dlrm_indexer_state(self.handle, ctypes.byref(st)))
+        return st.value
+
     def unique_rows(self, table):
         """0-based unique rows touched in `table` by the last build, in segment order (synchronises)."""
         n = ctypes.c_int64()
@@ -143,18 +149,25 @@ class SparseIndexer:
             pass
 
 
-def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, index_base=1, deterministic=True,
+def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, index_base=None, deterministic=True,
             prebuilt=False, check_bounds=True):
     """EmbeddingTables.update!(opt, tables, grads, indexers; num_splits, nthreads).
 
     `grads` are the SparseEmbeddingUpdates of maplookup_pullback (they share one gradient
     matrix and one PackedIndices, so all tables update in one launch).  num_splits/nthreads
     are accepted for signature parity; the GPU decomposition is chunk-based.
+    index_base: 1 (Julia) unless given; HipTables carry their own (a different one raises).
     Tables are mutated in place."""
     del num_splits, nthreads
     from .lazy import DeferredUpdate, HipTables, update_lazy
     if isinstance(tables, HipTables) and grads and isinstance(grads[0], DeferredUpdate):
+        tables.check_index_base(index_base, "update_")
+        if not deterministic:
+            raise ValueError("update_ on HipTables is the deterministic step apply (deterministic=False is not "
+                             "available on the fused path)")
+        # (indexers: accepted for the reference's signature; the step carries its own SparseIndexer)
         return update_lazy(opt, tables, grads, check_bounds=check_bounds)
+    index_base = 1 if index_base is None else int(index_base)
     if isinstance(tables, HipTables):
         tables = tables.ts
     if not isinstance(opt, Descent):

@@ -227,6 +227,12 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
                       int64_t* num_unique, int64_t* rows, int64_t* positions,
                       int64_t* seg_start, int64_t cap);
 
+/* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
+ * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only
+ * the repeated rows' gradients.  (The Julia shim's pullback state, DLRMHip.jl `st.bwd`.) */
+enum { DLRM_IX_BUILT = 1, DLRM_IX_SPLIT = 2, DLRM_IX_PREPARED = 4, DLRM_IX_SINGLES_DONE = 8 };
+int dlrm_indexer_state(const dlrm_indexer* indexer, unsigned* state);
+
 /* Backward of a training step without a materialized ys (see above). */
 int dlrm_interact_bwd_gather(dlrm_ctx* ctx, const dlrm_tables* tables, dlrm_indexer* indexer,
                              const void* indices, int itype, int64_t table_stride, int index_base,

@@ -142,9 +142,9 @@ def kaggle_tables(pkg, gpu, D, dtype, seed):
 
 @pytest.mark.parametrize("workload", ["kaggle-d128-b2048", "kaggle-d16-b2048", "kaggle-d128-b8192-bf16"])
 def test_bench_form_vs_oracle(pkg, gpu, workload):
-    """The exact step form bench.py times for each Kaggle-row workload (pkg.step_pipeline: the
-    metric config builds its indexer in the forward's launch, D = 16 in the previous step's apply
-    launch, bf16 B = 8192 on a side stream), over two consecutive batches so the prepared indexer is
+    """The exact step form bench.py times for each Kaggle-row workload (pkg.step_pipeline: B <= 2048,
+    the metric config and D = 16, build the next batch's indexer in the previous step's apply
+    launch; bf16 B = 8192 on a side stream), over two consecutive batches so the prepared indexer is
     consumed, at full table size, against the oracle on the touched rows (validation.jl:125-146)."""
     w = pkg.WORKLOADS[workload]
     D, B = w["dim"], w["batch"]

@@ -636,28 +636,33 @@ def test_prepare_with_unaligned_x_updates_once_hit_rows(pkg, gpu):
 def test_drop_in_operator_chain_on_step_kernels(pkg, gpu, rows, D, B, lr_known):
     """The reference's unchanged operator chain (maplookup -> rrule(DotInteraction) -> pullback ->
     maplookup_pullback -> update!) on HipTables runs the training-step kernels (3 launches, ys never
-    written) and equals HotPath.step bit for bit: out, dx, every table, over two steps."""
+    written) and equals HotPath.step bit for bit: out, dx, every table, over two steps.  The small
+    cases pass Julia's 1-based indices with every default left alone (HipTables, maplookup and
+    update_ all default to index_base = 1); the Kaggle case passes 0-based ones explicitly."""
+    base = 0 if rows == "kaggle" else 1
     if rows == "kaggle":
         rows = pkg.KAGGLE_EMBEDDING_SIZES
     rng = np.random.default_rng(B + D)
     T = len(rows)
     tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
-    idxs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+    idxs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1) + base).to(torch.int32).to(gpu))
             for _ in range(2)]
     x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
     F = T + 1
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
     lr = 0.25
-    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr if lr_known else None)
+    kw = {"index_base": 0} if base == 0 else {}
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr if lr_known else None, **kw)
     dot = pkg.DotInteraction()
     for p in idxs:
-        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p)
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p, **kw)
         assert isinstance(ys, pkg.LazyLookup) and ys.shape == (B, D + T * D)
         out, back = pkg.rrule(dot, x, ys)
         _, dx, dy = back(dout)
-        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), index_base=0)
+        assert dy.applied == lr_known
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), **kw)
     torch.cuda.synchronize()
-    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=0)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=base)
     for p in idxs:
         hp.step(x, p, dout)
     torch.cuda.synchronize()
@@ -665,12 +670,19 @@ def test_drop_in_operator_chain_on_step_kernels(pkg, gpu, rows, D, B, lr_known):
     assert np.array_equal(to_np_f32(dx), to_np_f32(hp.dx))
     for a, b in zip(ht.ts, hp.ts):
         assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+    # an index base other than the tables' own is refused, not silently shifted
+    with pytest.raises(ValueError):
+        pkg.maplookup(pkg.PreallocationStrategy(D), ht, idxs[0], index_base=1 - base)
     if lr_known:  # the pullback stepped the once-hit rows with η: update! must use the same η
         ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, idxs[0])
         _, back = pkg.rrule(dot, x, ys)
         _, _, dy = back(dout)
         with pytest.raises(ValueError):
-            pkg.update_(pkg.Descent(lr * 2), ht, pkg.maplookup_pullback(D, ht, idxs[0], dy), index_base=0)
+            pkg.update_(pkg.Descent(lr * 2), ht, pkg.maplookup_pullback(D, ht, idxs[0], dy), **kw)
+        # a second pullback of the same forward would step the once-hit rows twice: refused
+        with pytest.raises(pkg.DLRMError) as e:
+            back(dout)
+        assert e.value.code == pkg._lib.E_STATE
 
 
 def test_step_api_state_and_bounds(pkg, gpu):
@@ -816,7 +828,7 @@ def test_ys_backward_equals_gather_backward(pkg, gpu, T, D, B, dtype):
     a.check_bounds()
     assert torch.equal(a.out, g.out)
     assert torch.equal(a.dx, g.dx)
-    assert torch.equal(a.dt[:, D:], g.dt[:, D:])
+    assert torch.equal(a.dt, g.dt)  # x row included
 
 
 def test_fused_bounds_error(pkg, gpu):
