@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
                          "0: the engine's default (1: DESIGN.md §6)")
+    ap.add_argument("--shard-graph", choices=["full", "segments"], default="full",
+                    help="multi-GPU graph form: 'full' = one hipGraph per step with the RCCL all-to-alls "
+                         "inside (falls back to 'segments' where the capture is refused); 'segments' = the "
+                         "compute between eager collectives")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -57,6 +61,8 @@ def parse():
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
                          "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
     ap.add_argument("--stage-timing", type=int, default=1, help="0: skip the per-stage telemetry (traces)")
+    ap.add_argument("--ceiling", type=int, default=1,
+                    help="1: measure this box's stream and 512-B-row gather rates beside the 8 TB/s spec (rank 0)")
     ap.add_argument("--chain", type=int, default=1,
                     help="1: also time the reference's operator chain on HipTables (the drop-in path; one GPU)")
     ap.add_argument("--nbatch", type=int, default=NBATCH, help="distinct index batches cycled")
@@ -201,6 +207,44 @@ def cpu_baseline(pkg, w, seconds, threads):
                       f"reference (no julia toolchain)"}
 
 
+def measured_ceiling(dev, row_bytes):
+    """The HBM rates this box reaches, measured here beside the 8 TB/s spec (report both):
+    a 1 GiB device-to-device copy (read + write) and a gather of 262,144 random rows of `row_bytes`
+    from a 4 GiB buffer into a dense output (torch.index_select; read + write), each the best of 5
+    timed runs after a warm-up, on the current stream with HIP events.  tools/fetch_probe.hip is the
+    same measurement with PMC traffic (profiles/r6r_fetch_probe.json)."""
+    def best(fn, nbytes, reps=5):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t = []
+        for _ in range(reps):
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            t.append(e0.elapsed_time(e1) * 1e-3)
+        return round(nbytes / min(t) / 1e9, 1)
+    out = {}
+    try:
+        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        out["stream_copy_GBps"] = best(lambda: dst.copy_(src), 2 * src.numel() * 4)
+        del src, dst
+        cols = max(1, row_bytes // 4)
+        big = torch.empty((1 << 30) // cols, cols, dtype=torch.float32, device=dev)
+        idx = torch.randint(0, big.shape[0], (262144,), device=dev)
+        res = torch.empty((262144, cols), dtype=torch.float32, device=dev)
+        out["gather_GBps"] = best(lambda: torch.index_select(big, 0, idx, out=res), 2 * res.numel() * 4)
+        out["gather_row_bytes"] = cols * 4
+        out["method"] = ("best of 5 HIP-event-timed runs: 1 GiB copy (read+write); torch.index_select of 262,144 "
+                         "random rows from 4 GiB (read+write)")
+        del big, idx, res
+        torch.cuda.empty_cache()
+    except Exception as e:  # (memory / API trouble: reported, never fatal)
+        out["error"] = repr(e)
+    return out
+
+
 def load_prof(workload):
     """The committed rocprofv3 summary of this workload (tools/profile.sh -> profiles/pmc_<workload>.json:
     per-stage rocprof average durations, PMC HBM bytes and MFMA busy fractions, with the HEAD it was
@@ -280,17 +324,16 @@ def main():
         engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb,
                                                          micro=a.micro or None)
         if a.mode == "graph":
-            # the compute between the two all-to-alls is replayed as hipGraphs; the collectives
-            # are launched eagerly (RCCL inside hipGraph capture: not relied on)
+            # each whole step (both all-to-alls included) replayed as one hipGraph; where the
+            # backend refuses the capture, the compute between eager collectives
             for k in range(max(a.warmup, 1)):
                 step(k)
             torch.cuda.synchronize()
             try:
-                prepare_graphs()
-                a.mode = "segments"
+                a.mode = prepare_graphs(full=a.shard_graph == "full")
             except Exception as e:  # capture refused: eager launches (same work)
-                print(f"note: segment graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
-                engine._graphs = None
+                print(f"note: graph capture failed ({e!r}); timing eager launches", file=sys.stderr)
+                engine._graphs = engine._full = None
                 a.mode = "eager"
 
     # warm-up (also validates indices once)
@@ -586,6 +629,11 @@ def main():
                     "step": {"alg_bytes": int(step_bytes), "ms": round(ms, 4), "GBps": round(step_gbs, 1),
                              "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
                     "stages": stages}
+        if a.ceiling:
+            roofline["measured_ceiling"] = measured_ceiling(dev, D * E)
+            cg = roofline["measured_ceiling"].get("gather_GBps")
+            if cg:
+                roofline["frac_of_measured_gather"] = round(ach / cg, 4)
         if prof is not None:
             roofline["profile"] = {"file": f"profiles/pmc_{a.workload}.json", "head": prof.get("head"),
                                    "dominant_by": "rocprofv3 avg duration" if have else "HIP events",
@@ -623,6 +671,8 @@ def main():
                        "index_batches": nb,
                        **({"micro_batches": engine.M} if world > 1 else {}),
                        "launch": (f"hipGraph replay (<= {chunk} steps per graph)" if graphs is not None else
+                                  "hipGraph replay of each whole step, RCCL all-to-alls captured inside"
+                                  if a.mode == "full" else
                                   "hipGraph replay of the compute between eager all-to-alls" if a.mode == "segments"
                                   else "eager"),
                        "ys": ("received blocks read in place (no ys)" if world > 1 else "materialized"

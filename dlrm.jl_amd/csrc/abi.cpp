@@ -100,7 +100,7 @@ static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device
 static int step_parts_log2(int dflt = kStepParts) {
     const int forced = knobs().step_parts;
     const int p = forced > 0 ? forced : dflt;
-    return p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0));
+    return p >= 16 ? 4 : (p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0)));
 }
 
 static void record_build(dlrm_indexer* ix, bool split, const void* indices, int itype, int64_t tstride, int base,
@@ -109,6 +109,7 @@ static void record_build(dlrm_indexer* ix, bool split, const void* indices, int 
     ix->split = split;
     ix->prepared = false;
     ix->singles_done = false;
+    ix->dev.has_map = 0;  // (set by dlrm_step_bwd_prepare, whose wave build writes the item map)
     ix->indices = indices;
     ix->itype = itype;
     ix->tstride = tstride;
@@ -564,6 +565,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
         {(void**)&ix->prep_err, 16},
+        {(void**)&ix->dev.slice_rec, n * 32}, {(void**)&ix->dev.chunk_rec, n * 32},
+        {(void**)&ix->dev.item_tot, 16},     {(void**)&ix->dev.build_arrive, 16},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
         {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
         {(void**)&ix->dev.hseg, (size_t)(T0 * hs) * 8},
@@ -791,11 +794,13 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     }
     ix->prepared = false;
     ix->built = false;
-    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? step_parts_log2() : 0;
+    // the wave build in the forward's launch (vshift >= 2: it also writes the apply's item map)
+    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? step_parts_log2(kWaveBuildParts) : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev, tb->h_desc.data());
     if (rc == DLRM_OK) {
         record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+        ix->dev.has_map = ix->dev.vshift >= 2 ? 1 : 0;
         return DLRM_OK;
     }
     if (rc != DLRM_E_UNSUPPORTED) return rc;
@@ -934,10 +939,9 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
     next->built = false;
     next->prepared = false;
-    // 8 parts where the apply's rows are <= 256 B (D = 16 fp32; Terabyte bf16 x 128: 47.8M vs 45.2M
-    // samples/s with 4, profiles/r5d_*), 4 for the 512-B fp32 x 128 rows
-    const int row_bytes = tb->D * (tb->dtype == DLRM_F32 ? 4 : 2);
-    next->dev.vshift = step_parts_log2(row_bytes <= 256 ? kStepMaxParts : kStepParts);
+    // the wave build: kWaveBuildParts parts per table, one wave each (4 per workgroup: >= 4 parts)
+    next->dev.vshift = step_parts_log2(kWaveBuildParts);
+    if (next->dev.vshift < 2) next->dev.vshift = 2;
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
                       next->prep_err};
     rc = step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,
@@ -945,6 +949,7 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     if (rc) return rc;
     record_build(next, true, next_indices, itype, table_stride, index_base, batch, 1);
     next->prepared = true;
+    next->dev.has_map = 1;
     return DLRM_OK;
 }
 

@@ -22,6 +22,10 @@
 namespace dlrm {
 
 constexpr int kApplyThreads = 256;
+#ifndef DLRM_SLICE_IF
+#define DLRM_SLICE_IF 16
+#endif
+constexpr int kSliceIF = DLRM_SLICE_IF;  // hot slice: grad rows in flight per lane (16-B rows)
 constexpr int kApplyWaves = kApplyThreads / 64;
 
 // Lane-group geometry: D elements = VPR vectors of 16 B of the GRAD dtype; a group of LPR lanes
@@ -208,21 +212,24 @@ struct SliceLds {
     int last;
 };
 
-// ---- a slice of a hot segment, by the whole workgroup.  sd = {p0, p1, row, h}; hd = the
-// segment's {beg, end, row, s0}; vt = the (virtual) table whose arrays hold them.
+// ---- a slice of a hot segment, by the whole workgroup: pos = its positions (perm entries),
+// len of them, `row` the table row, `ns` the slices of its segment, its partial row at
+// part_me, the segment's first at part_first (slot spacing pdim), `cnt` the segment's arrival
+// counter (zero at rest).
 template <typename TT, typename GT, int VPR>
-__device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, const int4& sd, TT* __restrict__ table,
-                                          const GT* __restrict__ gbase, int64_t grad_ld, int L, float lr,
-                                          SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
+__device__ __forceinline__ void slice_body(const int32_t* __restrict__ pos, int len, TT* __restrict__ row, int ns,
+                                           float* part_me, const float* part_first, int64_t pdim, int32_t* cnt_p,
+                                           const GT* __restrict__ gbase, int64_t grad_ld, int L, float lr,
+                                           SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE, D = G::D, LPR = G::LPR, NG = G::NG;
     constexpr int SPG = (kHotSlice + NG - 1) / NG;  // positions per lane group
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int g = lane / LPR, v = lane % LPR, gid = w * G::RPW + g;
-    const int64_t off = (int64_t)vt * ix.cap;
-    const int len = sd.y - sd.x;
-    const int4 hd = ix.hot[off + sd.w];  // (needed only after the sums)
-    for (int i = tid; i < len; i += kApplyThreads) sm.pos[i] = ix.perm[off + sd.x + i];
+    // the table row, loaded now (needed only at the end; no other item writes it in this launch)
+    float rw[4];
+    if (tid < D / 4) load_row<TT, 4>(row, tid * 4, rw);
+    for (int i = tid; i < len; i += kApplyThreads) sm.pos[i] = pos[i];
     __syncthreads();
     // this group's consecutive share, in position order
     float acc[G::VPL][NE];
@@ -230,8 +237,11 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
     for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
         for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-    const int u1 = min(len, (gid + 1) * SPG);  // (SPG = kHotSlice / NG: two rounds of IF rows at D = 128)
-    constexpr int IF = G::IF < SPG ? G::IF : SPG;
+    const int u1 = min(len, (gid + 1) * SPG);  // (SPG = kHotSlice / NG)
+    // grad rows in flight per lane: a lane group's whole share at one 16-B vector per row
+    // up to kSliceIF, else the chunk items' IF
+    constexpr int IFS = G::VPL == 1 ? (SPG < kSliceIF ? SPG : kSliceIF) : G::IF;
+    constexpr int IF = IFS < SPG ? IFS : SPG;
     for (int u0 = gid * SPG; u0 < u1; u0 += IF) {
         typename Vec<GT>::type gv[IF][G::VPL];
 #pragma unroll
@@ -260,8 +270,6 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
                 sm.wsum[w][((v + j * 64) * NE + e) / 4] = f32x4{acc[j][e], acc[j][e + 1], acc[j][e + 2], acc[j][e + 3]};
     __syncthreads();
     // the waves, in wave order, by the first D/4 threads (one float4 of the row each)
-    const int ns = (hd.y - hd.x + kHotSlice - 1) / kHotSlice;
-    TT* row = table + (int64_t)(uint32_t)sd.z * D;
     f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
     if (tid < D / 4) {
 #pragma unroll
@@ -270,31 +278,28 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
     static_assert(D / 4 <= kApplyThreads, "a float4 of the row per thread");
     if (ns == 1) {
         if (tid < D / 4) {
-            float f[4];
-            load_row<TT, 4>(row, tid * 4, f);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) f[e] = __builtin_fmaf(-lr, sum[e], f[e]);
-            store_row<TT, 4>(row, tid * 4, f);
+            for (int e = 0; e < 4; ++e) rw[e] = __builtin_fmaf(-lr, sum[e], rw[e]);
+            store_row<TT, 4>(row, tid * 4, rw);
         }
         __syncthreads();  // sm reused by this workgroup's next item
         return;
     }
-    gi32_t* cnt = (gi32_t*)(ix.hot_cnt + off + sd.w);
-    if (tid < D / 4) store_sc1(ix.partial + ((int64_t)vt * ix.pcap + sl) * ix.pdim + tid * 4, sum);
+    gi32_t* cnt = (gi32_t*)cnt_p;
+    if (tid < D / 4) store_sc1(part_me + tid * 4, sum);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
     if (D / 4 > 64) __syncthreads();                   // (several storing waves)
     if (tid == 0) sm.last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
     __syncthreads();
     if (sm.last && tid < D / 4) {
-        float f[4];
-        load_row<TT, 4>(row, tid * 4, f);
-        const float* first = ix.partial + ((int64_t)vt * ix.pcap + hd.w) * ix.pdim + tid * 4;
+        float* f = rw;
+        const float* first = part_first + tid * 4;
         f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
         constexpr int PB = 16;  // partial rows in flight
         for (int k0 = 0; k0 < ns; k0 += PB) {
             f32x4 q[PB];
 #pragma unroll
-            for (int u = 0; u < PB; ++u) q[u] = load_sc1(first + (int64_t)(k0 + u < ns ? k0 + u : k0) * ix.pdim);
+            for (int u = 0; u < PB; ++u) q[u] = load_sc1(first + (int64_t)(k0 + u < ns ? k0 + u : k0) * pdim);
 #pragma unroll
             for (int u = 0; u < PB; ++u)
                 if (k0 + u < ns) s += q[u];
@@ -305,6 +310,33 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
         if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();  // sm reused by this workgroup's next item
+}
+
+// ---- a slice of a hot segment located by (virtual table vt, local slice sl): sd = {p0, p1,
+// row, h}; the segment's descriptor ix.hot[vt][h] = {beg, end, row, first slice}
+template <typename TT, typename GT, int VPR>
+__device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, const int4& sd, TT* __restrict__ table,
+                                          const GT* __restrict__ gbase, int64_t grad_ld, int L, float lr,
+                                          SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
+    constexpr int D = ApplyGeom<GT, VPR>::D;
+    const int64_t off = (int64_t)vt * ix.cap;
+    const int4 hd = ix.hot[off + sd.w];
+    const int ns = (hd.y - hd.x + kHotSlice - 1) / kHotSlice;
+    float* pbase = ix.partial + (int64_t)vt * ix.pcap * ix.pdim;
+    slice_body<TT, GT, VPR>(ix.perm + off + sd.x, sd.y - sd.x, table + (int64_t)(uint32_t)sd.z * D, ns,
+                            pbase + (int64_t)sl * ix.pdim, pbase + (int64_t)hd.w * ix.pdim, ix.pdim,
+                            ix.hot_cnt + off + sd.w, gbase, grad_ld, L, lr, sm);
+}
+
+// ---- flat hot slice k of the item map (one 32-B record: IndexerDev::slice_rec)
+template <typename TT, typename GT, int VPR>
+__device__ __forceinline__ void run_slice_rec(const IndexerDev& ix, int k, const int4& r0, const int4& r1,
+                                              TT* __restrict__ table, const GT* __restrict__ gbase, int64_t grad_ld,
+                                              int L, float lr, SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
+    constexpr int D = ApplyGeom<GT, VPR>::D;
+    slice_body<TT, GT, VPR>(ix.perm + r0.x, r0.y - r0.x, table + (int64_t)(uint32_t)r0.z * D, r1.x,
+                            ix.partial + (int64_t)k * ix.pdim, ix.partial + (int64_t)r1.y * ix.pdim, ix.pdim,
+                            ix.hot_cnt + r1.y, gbase, grad_ld, L, lr, sm);
 }
 
 }  // namespace dlrm

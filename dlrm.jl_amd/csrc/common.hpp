@@ -197,7 +197,13 @@ struct OutMap {
 constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions per table
 constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
 constexpr int kStepIndexMaxN = 2048;  // the forward-launch indexer (interact.hip): positions per table
-constexpr int kStepMaxParts = 8;      // ... which sorts a table as up to 8 parts (by the row's low bits)
+constexpr int kStepMaxParts = 16;     // ... which sorts a table as up to 16 parts (by the row's low bits)
+// the next batch's split build in the apply launch (indexer.hpp wave_build_group): parts per
+// table, one wave each, 4 per workgroup (>= 4)
+#ifndef DLRM_WAVE_PARTS
+#define DLRM_WAVE_PARTS 16
+#endif
+constexpr int kWaveBuildParts = DLRM_WAVE_PARTS;
 // split builds of kFastMaxN < N <= kPartsMaxN positions per table: the in-LDS build (1024
 // threads x 8 positions) over 2^kPartsLog2 parts per table (by the row's low bits), each part's
 // workgroup sized for the worst case (all N positions in one part); larger N: the hash build
@@ -237,6 +243,18 @@ struct IndexerDev {
     // indexed by v, and the apply maps v -> t.
     int vshift;
     int hbits;
+    // flat item lists of the wave build (apply.hpp reads them when has_map): every build wave
+    // reserves its hot slices and chunks with one atomic add per kind on build_arrive[2] / [1] and
+    // writes them whole; the last build workgroup (build_arrive[0] counts them in) copies the
+    // totals to item_tot = {hot slices, chunks} and resets the three counters.
+    //   slice_rec[2k, 2k+1]: {first perm entry, end (global: v * cap + local), row, v},
+    //                        {slices of its segment, flat index of the segment's first slice, 0, 0}
+    //   chunk_rec[2c, 2c+1]: the chunk descriptor (write_chunk) with global perm entries
+    int4* slice_rec;
+    int4* chunk_rec;
+    int32_t* item_tot;
+    uint32_t* build_arrive;  // [0] build workgroups arrived, [1] chunks, [2] hot slices reserved
+    int has_map;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)
     int pdim;              // partial row capacity (elements)

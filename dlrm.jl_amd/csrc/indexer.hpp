@@ -7,6 +7,9 @@
 #ifndef PHASE
 #define PHASE(k) do {} while (0)
 #endif
+#ifndef WPH
+#define WPH(k) do {} while (0)
+#endif
 
 namespace dlrm {
 
@@ -34,6 +37,16 @@ __device__ __forceinline__ void write_chunk(int4* chunks, int64_t c, int beg, in
     int q[kChunkInline];
 #pragma unroll
     for (int k = 0; k < kChunkInline; ++k) q[k] = (sorted_pos && beg + k < end) ? sorted_pos[beg + k] : -1;
+    chunks[2 * c] = make_int4(beg, end, row, q[0]);
+    chunks[2 * c + 1] = make_int4(q[1], q[2], q[3], q[4]);
+}
+
+// write_chunk with the descriptor's perm entries given apart from where its positions are read
+// (pos: the chunk's sorted positions, pos[0] its first)
+__device__ __forceinline__ void write_chunk_rec(int4* chunks, int64_t c, int beg, int end, int row, const int32_t* pos) {
+    int q[kChunkInline];
+#pragma unroll
+    for (int k = 0; k < kChunkInline; ++k) q[k] = beg + k < end ? pos[k] : -1;
     chunks[2 * c] = make_int4(beg, end, row, q[0]);
     chunks[2 * c + 1] = make_int4(q[1], q[2], q[3], q[4]);
 }
@@ -477,18 +490,34 @@ constexpr int kStepIndexEPL = kStepIndexMaxN / 256;  // positions per thread
 typedef FastLds<256, kStepIndexEPL, DLRM_STEP_DB> StepLds;
 
 // ------------------------------------------------- flat (table, item) lookup over counts
-// Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
-// may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.
+// Inclusive scan over the 64 lanes by DPP: Hillis-Steele inside each 16-lane row (row_shr 1, 2,
+// 4, 8), then the row totals (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).
+// Six VALU ops with no LDS permute (a __shfl_up chain is six dependent ds_bpermute round trips).
 __device__ __forceinline__ int wave_incl_scan(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
 }
 
+// The same scan with max (values >= 0): lane 63 holds the wave's maximum.
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
+__device__ __forceinline__ int lane63(int x) { return __builtin_amdgcn_readlane(x, 63); }
+
+// Flat id -> (table, offset) over per-table counts, T tables in tiles of 64 lanes.  Every lane
+// may carry its own id; shuffles run in uniform control flow.  table = -1 when id >= total.
 __device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb, int key, int& table, int& local) {
     // count of lanes with incl <= key (binary lifting over the non-decreasing prefix)
     int pos = 0;
@@ -508,7 +537,7 @@ __device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb,
 // of the G = ceil(T / 64) consecutive tables [l*G, l*G + G) and the inclusive prefix of their
 // sums, so a lookup is one binary lifting over the lanes plus G independent shuffles.  More
 // tables are re-scanned tile by tile on every lookup.
-constexpr int kScanTiles = 4;
+constexpr int kScanTiles = 8;  // (T <= 512 virtual tables: the wave build's 16 parts of up to 32 tables)
 struct TableScan {
     int cnt[kScanTiles];  // counts of this lane's tables
     int incl;             // inclusive prefix over the lanes' groups
@@ -529,7 +558,7 @@ __device__ __forceinline__ TableScan scan_counts(const IndexerDev& ix, int T_, i
             sum += r.cnt[q];
         }
         r.incl = wave_incl_scan(sum);
-        r.total = __shfl(r.incl, 63, 64);
+        r.total = lane63(r.incl);
         return r;
     }
     for (int tb = 0; tb < T_; tb += 64) {
@@ -576,5 +605,366 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
     }
 }
 
+
+// ------------------------------------------------------------- wave build (round 4)
+// The training step's split build of the NEXT batch, by ONE WAVE per virtual table (t, part):
+// no workgroup barrier after the first.  The 256-thread block build (fast_index_table) took
+// ~12 us per part inside the apply launch: ~15 dependent barrier + LDS phases with one wave per
+// SIMD, its length the same alone, beside the apply, or run twice on a warm instruction cache
+// (tools/phase_step.py, profiles/r10_apply_timeline.txt).  Here a workgroup's 4 waves take 4
+// consecutive parts of one table -- their keys together are at most the table's N positions,
+// so one pool sized for N holds them, each wave taking its share by an LDS cursor -- and each
+// wave sorts ~N/16 keys with wave-level steps only.
+// Output format = fast_index_table's (split): the apply, dlrm_indexer_read and the step backward
+// read it unchanged.  Within a part, segments come in ascending row order, positions ascending.
+constexpr int kWaveParts = 4;       // waves per build workgroup = parts of one table per workgroup
+constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-byte bucket is this small
+constexpr int kApplyMapThreads = kWaveParts * 64;  // the workgroup that writes the item map
+struct WaveBuildLds {
+    uint32_t K[2][kStepIndexMaxN];  // keys (row >> vshift), sort ping-pong; pool shared by the 4 waves
+    int32_t V[2][kStepIndexMaxN];   // positions
+    int32_t R[kStepIndexMaxN];      // per-key rank in its digit, then segment starts
+    uint32_t cnt[kWaveParts][256];  // per-wave digit counters, then digit offsets
+    int cursor;                     // pool allocation
+};
+
+__device__ __forceinline__ unsigned long long lanes_below() {
+    const int lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// Lanes (among `ok` ones) whose `bits`-bit digit (bits <= 8, uniform) equals this lane's.
+__device__ __forceinline__ unsigned long long match_digit(uint32_t d, bool ok, int bits) {
+    unsigned long long peers = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        if (bit >= bits) break;  // uniform
+        const unsigned long long bb = __ballot(ok && ((d >> bit) & 1u));
+        peers &= ((d >> bit) & 1u) ? bb : ~bb;
+    }
+    return peers;
+}
+
+// One stable counting pass of one wave over keys [0, n) of (Kin, Vin), on the `bits`-bit digit
+// at `shift`, into (Kout, Vout).  Tiles of 64 keys in order; in a tile, the lanes sharing a digit
+// are found by ballots and the group's first lane adds the group's size to the digit's counter
+// with one LDS atomic, whose old value is the group's base (a wave's LDS operations complete in
+// order, so the bases follow the tiles).  Leaves cnt[d] = the start of digit d's bucket; returns
+// the largest bucket.
+__device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
+                               int32_t* Vout, int32_t* R, uint32_t* cnt) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lanes_below();
+    const uint32_t dm = (1u << bits) - 1u;
+    *(uint4*)&cnt[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
+    wave_lds_sync();
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int i = j0 + lane;
+        const bool ok = i < n;
+        const uint32_t d = ok ? (Kin[i] >> shift) & dm : 0u;
+        const unsigned long long peers = match_digit(d, ok, bits);
+        const int rank = __popcll(peers & lt);
+        uint32_t old = 0;
+        if (ok && rank == 0) old = atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+        const int leader = ok ? __ffsll((long long)peers) - 1 : lane;
+        const uint32_t b = (uint32_t)__shfl((int)old, leader, 64);
+        if (ok) R[i] = (int)b + rank;
+    }
+    wave_lds_sync();
+    const uint4 c = *(const uint4*)&cnt[4 * lane];  // lane l: digits 4l .. 4l+3
+    const int sum = (int)(c.x + c.y + c.z + c.w);
+    int o = wave_incl_scan(sum) - sum;
+    uint4 st;
+    st.x = o; o += c.x;
+    st.y = o; o += c.y;
+    st.z = o; o += c.z;
+    st.w = o;
+    *(uint4*)&cnt[4 * lane] = st;
+    const int m = lane63(wave_incl_max((int)max(max(c.x, c.y), max(c.z, c.w))));
+    wave_lds_sync();
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int i = j0 + lane;
+        if (i < n) {
+            const uint32_t k = Kin[i];
+            const int dst = (int)cnt[(k >> shift) & dm] + R[i];
+            Kout[dst] = k;
+            Vout[dst] = Vin[i];
+        }
+    }
+    wave_lds_sync();
+    return m;
+}
+
+// Every low-byte bucket small (uniform rows): each key's place in its bucket by a direct rank on
+// (key, position); the stable pass left each bucket in position order, so j < i <=> pos_j < pos_i.
+__device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, uint32_t* K0, int32_t* V0,
+                                  const uint32_t* start) {
+    for (int i = threadIdx.x & 63; i < n; i += 64) {
+        const uint32_t ki = K1[i];
+        const int d = ki & 255u;
+        const int bs = (int)start[d], be = d < 255 ? (int)start[d + 1] : n;
+        int rank = 0;
+        for (int j = bs; j < be; ++j) {
+            const uint32_t kj = K1[j];
+            rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+        }
+        K0[bs + rank] = ki;
+        V0[bs + rank] = V1[i];
+    }
+    wave_lds_sync();
+}
+
+// Virtual table v = (t << vs) + part of the split build, by the calling wave (w = its index in
+// the workgroup); sl.cursor was zeroed before a workgroup barrier.  Lane l reads positions
+// [32 l, 32 l + 32) of the table (one contiguous 128-B run: 16-B loads), so the part's keys are
+// compacted in position order by one wave scan of the lanes' counts, with no per-tile ballot.
+__device__ void wave_index_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows,
+                                const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
+                                unsigned* __restrict__ err, WaveBuildLds& sl, int w) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lanes_below();
+    const uint32_t pmask = (1u << vs) - 1u, part = (uint32_t)v & pmask;
+    const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
+    const int nbits = 32 - __clz(kmax);
+    constexpr int E = kStepIndexMaxN / 64;  // positions per lane
+    constexpr int KB = E / 4;               // 16-B pieces per lane: piece k covers positions
+                                            // [256 k + 4 lane, +4) (wave-coalesced, 1 KB per load)
+    WPH(0);
+    // the lane's E indices: 16-B loads when whole and aligned, else one by one; each validated
+    // (0 <= row < nrows; out of range raises BoundsError, part 0 reports it) and kept when it is
+    // this part's.  Element j = 4 k + e is position 256 k + 4 lane + e.
+    uint32_t rv[E];       // row (32-bit)
+    uint32_t keep = 0;    // bit j: element j is this part's
+    bool bad = false;
+    {
+        const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+        const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
+        const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
+        if (vec && itype == DLRM_I32) {
+            int4 q[KB];
+#pragma unroll
+            for (int k = 0; k < KB; ++k)
+                if (256 * k < N) q[k] = ldg<int4>(i32 + 256 * k + 4 * lane);  // (uniform guard)
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                if (256 * k >= N) break;
+                const int32_t e4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t r = (int64_t)e4[e] - base;
+                    const bool ok = (uint64_t)r < (uint64_t)nrows;  // (negative: a huge unsigned)
+                    bad |= !ok;
+                    keep |= (ok && ((uint32_t)r & pmask) == part) ? (1u << (4 * k + e)) : 0u;
+                    rv[4 * k + e] = (uint32_t)r;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const int pj = 256 * (j >> 2) + 4 * lane + (j & 3);
+                const bool in = pj < N;
+                const int64_t r = load_index_if(in, idx, itype, (int64_t)t * tstride + pj) - base;
+                const bool ok = in && r >= 0 && r < (int64_t)nrows;
+                bad |= in && !ok;
+                keep |= (ok && ((uint32_t)r & pmask) == part) ? (1u << j) : 0u;
+                rv[j] = (uint32_t)r;
+            }
+        }
+    }
+    if (part == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    // compaction in position order (piece k of every lane before piece k + 1): per piece a DPP
+    // scan of the lanes' kept counts
+    int kbase[KB];
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        const int c = __popc((keep >> (4 * k)) & 0xfu);
+        const int incl = wave_incl_scan(c);
+        kbase[k] = n + incl - c;
+        n += lane63(incl);
+    }
+    WPH(1);
+    int pb = 0;
+    if (lane == 0) pb = atomicAdd(&sl.cursor, n);
+    pb = __builtin_amdgcn_readfirstlane(pb);
+    uint32_t* K0 = sl.K[0] + pb;
+    uint32_t* K1 = sl.K[1] + pb;
+    int32_t* V0 = sl.V[0] + pb;
+    int32_t* V1 = sl.V[1] + pb;
+    int32_t* R = sl.R + pb;
+    uint32_t* cnt = sl.cnt[w];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        int q = kbase[k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if ((keep >> (4 * k + e)) & 1u) {
+                K0[q] = rv[4 * k + e] >> vs;
+                V0[q] = 256 * k + 4 * lane + e;
+                ++q;
+            }
+    }
+    wave_lds_sync();
+    WPH(2);
+    const uint32_t* Ks = K0;
+    const int32_t* Vs = V0;
+    if (n > 1 && nbits > 0) {
+        const int mb = wave_count_pass(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
+        WPH(3);
+        Ks = K1;
+        Vs = V1;
+        if (nbits > 8) {
+            if (mb <= kWaveRankMax) {
+                wave_rank_buckets(n, K1, V1, K0, V0, cnt);
+                Ks = K0;
+                Vs = V0;
+            } else {  // skewed rows: the remaining LSD passes
+                for (int shift = 8; shift < nbits; shift += 8) {
+                    const bool from1 = Ks == K1;
+                    wave_count_pass(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
+                                    from1 ? K0 : K1, from1 ? V0 : V1, R, cnt);
+                    Ks = from1 ? K0 : K1;
+                    Vs = from1 ? V0 : V1;
+                }
+            }
+        }
+    }
+    WPH(4);
+    // segments: perm, seg_start / seg_row, once-hit flags; segment starts kept in R
+    const int64_t off = (int64_t)v * ix.cap;
+    int32_t* perm = ix.perm + off;
+    int32_t* seg_start = ix.seg_start + (int64_t)v * (ix.cap + 1);
+    uint32_t* seg_row = ix.seg_row + off;
+    uint8_t* single = ix.single + (int64_t)t * ix.cap;
+    int U = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int i = j0 + lane;
+        const bool ok = i < n;
+        const uint32_t k = ok ? Ks[i] : 0u;
+        const bool head = ok && (i == 0 || Ks[i - 1] != k);
+        const bool tail = ok && (i + 1 == n || Ks[i + 1] != k);
+        if (ok) {
+            const int p = Vs[i];
+            perm[i] = p;
+            single[p] = (head && tail) ? 1 : 0;
+        }
+        const unsigned long long hb = __ballot(head);
+        if (head) {
+            const int s = U + __popcll(hb & lt);
+            seg_start[s] = i;
+            seg_row[s] = (k << vs) | part;
+            R[s] = i;
+        }
+        U += __popcll(hb);
+    }
+    if (lane == 0) seg_start[U] = n;
+    wave_lds_sync();
+    WPH(5);
+    // chunks (2 ..kChunk positions; once-hit positions are the backward's), hot segments + slices:
+    // per virtual table (dlrm_indexer_read, the counts-scanning apply), then, with this wave's
+    // range of the flat lists reserved by one atomic add per kind, as flat records (the
+    // item-map apply: one load per item)
+    int4* chunks = ix.chunks + 2 * off;
+    int4* hot = ix.hot + off;
+    int4* hot_slice = ix.hot_slice + off;
+    int C = 0, H = 0, S = 0;
+    for (int s0 = 0; s0 < U; s0 += 64) {
+        const int s = s0 + lane;
+        const bool ok = s < U;
+        const int beg = ok ? R[s] : 0;
+        const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
+        const int len = end - beg;
+        const bool isc = ok && len >= 2 && len <= kChunk;
+        const bool ish = ok && len > kChunk;
+        const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
+        const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
+        const int sincl = wave_incl_scan(ns);
+        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
+        if (isc) write_chunk(chunks, C + __popcll(cb & lt), beg, end, row, Vs);
+        if (ish) {
+            const int h = H + __popcll(hb & lt), s0s = S + sincl - ns;
+            hot[h] = make_int4(beg, end, row, s0s);
+            write_slices(hot_slice, s0s, beg, end, row, h);
+        }
+        C += __popcll(cb);
+        H += __popcll(hb);
+        S += lane63(sincl);
+    }
+    if (lane == 0) {
+        int32_t* cn = ix.counts + (int64_t)v * 8;
+        cn[CNT_U] = U; cn[CNT_C] = C; cn[CNT_H] = H; cn[CNT_S] = S; cn[CNT_NV] = n;
+    }
+    if (C + S > 0) {
+        unsigned cbase = 0, sbase = 0;
+        if (lane == 0) {
+            if (C) cbase = __hip_atomic_fetch_add(ix.build_arrive + 1, (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (S) sbase = __hip_atomic_fetch_add(ix.build_arrive + 2, (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        cbase = __builtin_amdgcn_readfirstlane(cbase);
+        sbase = __builtin_amdgcn_readfirstlane(sbase);
+        int c = 0, sl = 0;
+        for (int s0 = 0; s0 < U; s0 += 64) {
+            const int s = s0 + lane;
+            const bool ok = s < U;
+            const int beg = ok ? R[s] : 0;
+            const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
+            const int len = end - beg;
+            const bool isc = ok && len >= 2 && len <= kChunk;
+            const bool ish = ok && len > kChunk;
+            const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
+            const unsigned long long cb = __ballot(isc);
+            const int sincl = wave_incl_scan(ns);
+            const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
+            if (isc) {  // the descriptor with global perm entries (v * cap + local)
+                const int64_t f = (int64_t)cbase + c + __popcll(cb & lt);
+                write_chunk_rec(ix.chunk_rec, f, (int)(off + beg), (int)(off + end), row, Vs + beg);
+            }
+            if (ish) {
+                const int first = (int)sbase + sl + sincl - ns;
+                for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
+                    ix.slice_rec[2 * (int64_t)(first + k)] =
+                        make_int4((int)(off + p0), (int)(off + min(p0 + kHotSlice, end)), row, v);
+                    ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
+                }
+            }
+            c += __popcll(cb);
+            sl += lane63(sincl);
+        }
+    }
+    WPH(6);
+}
+
+// The last build workgroup: the flat lists' totals (every wave's reservation add returned before
+// its workgroup arrived), then the counters reset for this indexer's next build (a later launch).
+__device__ void finish_item_lists(const IndexerDev& ix) {
+    if (threadIdx.x == 0) {
+        const unsigned c = __hip_atomic_load(ix.build_arrive + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned s = __hip_atomic_load(ix.build_arrive + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ix.item_tot[0] = (int)s;
+        ix.item_tot[1] = (int)c;
+        ix.build_arrive[0] = 0u;
+        ix.build_arrive[1] = 0u;
+        ix.build_arrive[2] = 0u;
+    }
+}
+
+// One build workgroup (kWaveParts waves = 256 threads): parts g*4 .. g*4+3 of table (g*4) >> vs
+// (vs >= 2) of T tables.  Every thread of the workgroup calls it.  The last of the T << vs >> 2
+// workgroups to arrive (one agent-scope add per workgroup, after its waves' reservation adds have
+// returned) publishes the flat lists' totals (finish_item_lists).
+__device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
+                                 const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
+                                 unsigned* __restrict__ err, WaveBuildLds& sl) {
+    if (threadIdx.x == 0) sl.cursor = 0;
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    const int v = g * kWaveParts + w, t = v >> ix.vshift;
+    wave_index_part(ix, v, t, ix.vshift, (uint32_t)load_table(tabs, t).nrows, idx, itype, tstride, base, N, err, sl, w);
+    const int groups = (T << ix.vshift) / kWaveParts;
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(ix.build_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(groups - 1))
+        finish_item_lists(ix);
+}
 
 }  // namespace dlrm

@@ -254,7 +254,10 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
                                                                  TabPtrs tp) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int T_ = F - 1;
-    const int NI = T_ << ix.vshift;
+    // vshift >= 2: the wave build (indexer.hpp wave_build_group: 4 parts per workgroup, one wave
+    // each, and the flat item map); else the block build, one workgroup per table part
+    const bool wave = ix.vshift >= 2;
+    const int NI = wave ? (T_ << ix.vshift) / kWaveParts : T_ << ix.vshift;
 #ifdef DLRM_PHASE
     // [0] this block's start (the traced indexer block), [60] / [61] first start / last end of any
     // gather block, [62] / [63] first start / last end of any indexer block
@@ -265,10 +268,15 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
     }
 #endif
     if ((int)blockIdx.x < NI) {
-        StepLds& sl = *(StepLds*)smem;
-        const int v = blockIdx.x, t = v >> ix.vshift;
-        fast_index_table<256, kStepIndexEPL, true>(ix, v, t, ix.vshift, (uint32_t)ga.tabs[t].nrows, ga.idx, ga.itype,
-                                                   ga.tstride, ga.base, B * ga.L, ga.err, sl);
+        if (wave) {
+            wave_build_group(ix, blockIdx.x, T_, ga.tabs, ga.idx, ga.itype, ga.tstride, ga.base, B * ga.L, ga.err,
+                             *(WaveBuildLds*)smem);
+        } else {
+            StepLds& sl = *(StepLds*)smem;
+            const int v = blockIdx.x, t = v >> ix.vshift;
+            fast_index_table<256, kStepIndexEPL, true>(ix, v, t, ix.vshift, (uint32_t)ga.tabs[t].nrows, ga.idx,
+                                                       ga.itype, ga.tstride, ga.base, B * ga.L, ga.err, sl);
+        }
 #ifdef DLRM_PHASE
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&g_phase_fwd[63], wall_clock64());
@@ -840,7 +848,8 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : (NB > 2 ? 2 : 4)) vo
 #pragma unroll
                         for (int e = 0; e < CPL; ++e) wv[e] = __builtin_fmaf(-su.lr, 0.0f + v[e], tw[e]);
                         store_row<T, CPL, true>((T*)tds[f - 1].data + (int64_t)urow[I][r] * d, n0, wv);
-                    } else if constexpr (!mapped) {
+                    } else if (!mapped && (f > 0 || !su.single)) {
+                        // (the training step (su.single set) leaves dt's x row alone: dx carries it)
                         // (CPL = 8: a lane's two 16-B pieces are 32 B apart, so each store instruction
                         // covers half of every line: plain stores let L2 merge the halves, where
                         // non-temporal ones left as partial-line writes, 95 -> 117 MB per launch)
@@ -1240,9 +1249,11 @@ int launch_step_fwd(dlrm_ctx* ctx, const TableDesc* tabs, bool tabs_aligned16, i
     GatherArgs ga{tabs, idx, itype, tstride, base, 1, ctx_error_word(ctx)};
     TabPtrs tp{};
     if (!fill_tab_ptrs(tp, htabs, T_)) return DLRM_E_UNSUPPORTED;
-    size_t lds = sizeof(StepLds);
+    const bool wave = ix.vshift >= 2;
+    size_t lds = wave ? sizeof(WaveBuildLds) : sizeof(StepLds);
     if (lds < sizeof(float) * 4 * kStage) lds = sizeof(float) * 4 * kStage;
-    const unsigned g = grid_for(B, fwd_samples_per_block(d, NB), cus) + (T_ << ix.vshift);
+    const unsigned g = grid_for(B, fwd_samples_per_block(d, NB), cus) +
+                       (wave ? (T_ << ix.vshift) / kWaveParts : (T_ << ix.vshift));
 #define DLRM_LAUNCH_FWDIX(TY, N_)                                                                                  \
     if (d == 128)                                                                                                  \
         hipLaunchKernelGGL((interact_fwd_index_kernel<TY, N_, 128>), dim3(g), dim3(256), lds, s, d, F, B,            \

@@ -33,6 +33,11 @@ __device__ unsigned long long g_blk[2][256];
 __device__ unsigned long long g_phase2[256][32];  // every block < 256: marks k < 32
 #define PHASE(k) do { __syncthreads(); if (threadIdx.x == 0) { const unsigned long long c_ = wall_clock64(); \
     if (blockIdx.x == DLRM_PHASE) g_phase[k] = c_; if (blockIdx.x < 256 && (k) < 32) g_phase2[blockIdx.x][k] = c_; } } while (0)
+__device__ unsigned long long g_wph[256][4][16];  // wave build: per block, wave, mark
+#define WPH(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_wph[blockIdx.x][(threadIdx.x >> 6) & 3][k] = wall_clock64(); } while (0)
+extern "C" int dlrm_debug_wph(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wph), sizeof(g_wph));
+}
 extern "C" int dlrm_debug_phase2(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase2), sizeof(g_phase2));
 }
@@ -361,31 +366,46 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     int bid = blockIdx.x, nblk = gridDim.x;
     if (MODE == 2) {
         extern __shared__ __attribute__((aligned(16))) unsigned char prep_lds[];
-        const int NI = pa.T << pa.ix.vshift;
-        if (bid < NI) {
-            const int vv = bid, t = vv >> pa.ix.vshift;
-            ITEM_START(4, 0, vv);
-            fast_index_table<256, kStepIndexEPL, true>(pa.ix, vv, t, pa.ix.vshift, (uint32_t)load_table(pa.tabs, t).nrows,
-                                                       pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
-                                                       *(StepLds*)prep_lds);
+        const int NI = (pa.T << pa.ix.vshift) / kWaveParts;
+        if (bid < NI) {  // the next batch's split build: one wave per table part (indexer.hpp)
+            ITEM_START(4, 0, bid);
+            wave_build_group(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
+                             *(WaveBuildLds*)prep_lds);
             ITEM_END(0);
             return;
         }
         bid -= NI;
         nblk -= NI;
+#ifdef DLRM_PREP_ONLY  // (probe: the build alone in this launch)
+        return;
+#endif
     }
     // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
-    // this step): the reference's gather throws before update!, so no table row is written
-    if (*err) return;
+    // this step): the reference's gather throws before update!, so no table row is written.  (The
+    // error word is loaded with the item counts, one round trip for both.)
+    const unsigned err0 = ldg<unsigned>(err);
     typedef ApplyGeom<GT, VPR> G;
     constexpr int D = G::D, NG = G::NG;
     __shared__ SliceLds<D> sm;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane / G::LPR, v = lane % G::LPR;
     const int gid = w * G::RPW + g;
-    const TableScan sS = scan_counts(ix, T_, CNT_S);
-    const TableScan sC = scan_counts(ix, T_, CNT_C);
-    const int citems = sS.total + (sC.total + NG - 1) / NG;
+    // where this launch's items are: the wave build's flat item map (one load per item), else a
+    // wave scan of every virtual table's counts (TableScan) and a lookup in it per item
+    const bool mp = ix.has_map != 0;
+    TableScan sS{}, sC{};
+    int Stot, Ctot;
+    if (mp) {
+        Stot = ix.item_tot[0];
+        Ctot = ix.item_tot[1];
+    } else {
+        sS = scan_counts(ix, T_, CNT_S);
+        sC = scan_counts(ix, T_, CNT_C);
+        Stot = sS.total;
+        Ctot = sC.total;
+    }
+    if (err0) return;
+    const int citems = Stot + (Ctot + NG - 1) / NG;
     constexpr int SP = NG * G::SPPG;                           // positions per singles item
     const int per_t = SG ? (sa.N + SP - 1) / SP : 0;          // singles items per real table
     const int items = citems + (T_ >> ix.vshift) * per_t;
@@ -398,13 +418,13 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     //   item = pos + (pos < e0 ? r0 : pos < e1 ? s1 : s2), pos = this workgroup's list position
     int pos0 = bid, step = nblk, npos = items, r0 = 0, e0 = items, s1 = 0, e1 = items, s2 = 0;
     if (L > 1 && (nblk & 7) == 0 && ((blockIdx.x - bid) & 7) == 0) {
-        const int x = bid & 7, c1 = citems - sS.total, c2 = items - citems;
-        const int a0 = (int)((int64_t)sS.total * x >> 3), b0 = (int)((int64_t)sS.total * (x + 1) >> 3);
+        const int x = bid & 7, c1 = citems - Stot, c2 = items - citems;
+        const int a0 = (int)((int64_t)Stot * x >> 3), b0 = (int)((int64_t)Stot * (x + 1) >> 3);
         const int a1 = (int)((int64_t)c1 * x >> 3), b1 = (int)((int64_t)c1 * (x + 1) >> 3);
         const int a2 = (int)((int64_t)c2 * x >> 3), b2 = (int)((int64_t)c2 * (x + 1) >> 3);
         r0 = a0;
         e0 = b0 - a0;
-        s1 = sS.total + a1 - e0;
+        s1 = Stot + a1 - e0;
         e1 = e0 + (b1 - a1);
         s2 = citems + a2 - e1;
         npos = e1 + (b2 - a2);
@@ -416,10 +436,10 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
 #endif
     for (int pos = pos0; pos < npos; pos += step) {
         const int item = pos + (pos < e0 ? r0 : (pos < e1 ? s1 : s2));
-        APPLY_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2));
+        APPLY_START(item >= citems ? 3 : (item >= Stot ? 1 : 2));
 #ifdef DLRM_PHASE
         const int k_ = kk_++;
-        ITEM_START(item >= citems ? 3 : (item >= sS.total ? 1 : 2), k_, item);
+        ITEM_START(item >= citems ? 3 : (item >= Stot ? 1 : 2), k_, item);
 #undef APPLY_END
 #define APPLY_END() do { ITEM_END(k_); } while (0)
 #endif
@@ -433,15 +453,37 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
             APPLY_END();
             continue;
         }
-        if (item >= sS.total) {
-            int tc, cl;
-            locate(ix, T_, CNT_C, sC, (item - sS.total) * NG + gid, tc, cl);
-            if (g >= G::RPW || tc < 0) continue;
-            const int64_t co = 2 * ((int64_t)tc * ix.cap + cl);
-            const int4 ca = ix.chunks[co], cb = ix.chunks[co + 1];
-            const int t = tc >> ix.vshift;
-            run_chunk<TT, GT, VPR>(ix.perm + (int64_t)tc * ix.cap, ca, cb, (TT*)tabs[t].data,
-                                   grad + grad_offset + (int64_t)t * D, grad_ld, L, lr, v, lane - v);
+        if (item >= Stot) {
+            const int fc = (item - Stot) * NG + gid;  // flat chunk of this lane group
+            const int32_t* pbase;
+            int4 ca, cb;
+            int t;
+            if (mp) {  // the flat chunk record: perm entries global, the virtual table = beg / cap
+                if (g >= G::RPW || fc >= Ctot) continue;
+                ca = ix.chunk_rec[2 * (int64_t)fc];
+                cb = ix.chunk_rec[2 * (int64_t)fc + 1];
+                pbase = ix.perm;
+                t = (int)(ca.x / ix.cap) >> ix.vshift;
+            } else {
+                int tc, cl;
+                locate(ix, T_, CNT_C, sC, fc, tc, cl);
+                if (g >= G::RPW || tc < 0) continue;
+                const int64_t co = 2 * ((int64_t)tc * ix.cap + cl);
+                ca = ix.chunks[co];
+                cb = ix.chunks[co + 1];
+                pbase = ix.perm + (int64_t)tc * ix.cap;
+                t = tc >> ix.vshift;
+            }
+            run_chunk<TT, GT, VPR>(pbase, ca, cb, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, L,
+                                   lr, v, lane - v);
+            APPLY_END();
+            continue;
+        }
+        if (mp) {  // (uniform: the slice's whole record in one 32-B load)
+            const int4 r0 = ix.slice_rec[2 * (int64_t)item], r1 = ix.slice_rec[2 * (int64_t)item + 1];
+            const int t = r0.w >> ix.vshift;
+            run_slice_rec<TT, GT, VPR>(ix, item, r0, r1, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D,
+                                       grad_ld, L, lr, sm);
             APPLY_END();
             continue;
         }
@@ -462,17 +504,18 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
 // The step indexer's workgroups alone (PrepArgs), where the apply has no vector kernel to host them.
 __global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int vv = blockIdx.x, t = vv >> pa.ix.vshift;
-    fast_index_table<256, kStepIndexEPL, true>(pa.ix, vv, t, pa.ix.vshift, (uint32_t)load_table(pa.tabs, t).nrows,
-                                               pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err, *(StepLds*)lds);
+    wave_build_group(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
+                     *(WaveBuildLds*)lds);
 }
 
 // step_index_kernel's own launch (the next batch's split build when the apply launch cannot carry it)
 static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
     static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(StepLds));
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(WaveBuildLds));
     (void)attr;
-    hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)(pa.T << pa.ix.vshift)), dim3(256), sizeof(StepLds), s, pa);
+    hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)((pa.T << pa.ix.vshift) / kWaveParts)), dim3(256),
+                       sizeof(WaveBuildLds), s, pa);
 }
 
 // Generic (any D) versions: one thread per element column.
@@ -647,11 +690,11 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     if (pa && !sa.single) {
         static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           (int)sizeof(StepLds));
+                                                           (int)sizeof(WaveBuildLds));
         (void)attr;
-        const int NI = pa->T << pa->ix.vshift;
+        const int NI = (pa->T << pa->ix.vshift) / kWaveParts;
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
-                           sizeof(StepLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
+                           sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
                            *pa);
     } else if (sa.single) {
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 1>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,

@@ -417,7 +417,7 @@ function train_step_fwd!(st::HipTrainStep{T}, x::AbstractMatrix{T}, sparse) wher
                          Ptr{Cvoid}, Int64, Cint),
                         st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
                         st.x.ptr, d, st.out.ptr, size(st.out, 1), st.padding))
-    return Array(st.out)
+    return x isa DeviceMatrix ? st.out : Array(st.out)   # device-resident when the caller's x is
 end
 
 """
@@ -425,11 +425,12 @@ end
 
 With `next` (the next batch's sparse features) the step's apply launch also builds the next
 batch's indexer (dlrm_step_bwd_prepare), so `train_step_fwd!(st, x_next, next)` only gathers.
-Results are identical either way.
+Results are identical either way.  A `DeviceMatrix` Δ is read in place and `dx` comes back as
+the step's `DeviceMatrix` (no PCIe copy either way); a host Δ is uploaded and `dx` downloaded.
 """
 function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}; next = nothing) where {T}
     d, B = size(st.x)
-    Δd = upload!(DeviceMatrix{T}(st.ctx, size(Δ)...), Matrix{T}(Δ))
+    Δd = Δ isa DeviceMatrix ? Δ : upload!(DeviceMatrix{T}(st.ctx, size(Δ)...), Matrix{T}(Δ))
     if next !== nothing
         nidx = next isa PackedIndices ? next : pack(st.ctx, next)
         nidx.batch == st.idx.batch || throw(DimensionMismatch("the next batch must have the same size"))
@@ -443,7 +444,7 @@ function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}; next = noth
                             size(st.dt, 1), st.lr, nix.ptr, nidx.data.ptr, Cuint(0)))
         st.spare, st.ix = st.ix, nix
         st.pending = next => nidx
-        return Array(st.dx)
+        return Δ isa DeviceMatrix ? st.dx : Array(st.dx)
     end
     check(st.ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
@@ -451,7 +452,7 @@ function train_step_bwd!(st::HipTrainStep{T}, Δ::AbstractMatrix{T}; next = noth
                         st.ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
                         st.x.ptr, d, Δd.ptr, size(Δ, 1), st.padding, st.dx.ptr, d, st.dt.ptr, size(st.dt, 1),
                         st.lr, Cuint(0)))
-    return Array(st.dx)
+    return Δ isa DeviceMatrix ? st.dx : Array(st.dx)
 end
 
 #####
@@ -505,8 +506,10 @@ function _fused_interact(dot::HipDotInteraction, x::AbstractMatrix{T}, ys::HipLo
     return st
 end
 
+# (a DeviceMatrix x -- the bottom MLP on the GPU -- gets the DeviceMatrix out: no PCIe copy)
 (dot::HipDotInteraction)(x::AbstractMatrix{T}, ys::HipLookup{T}; return_t = false) where {T} =
-    return_t ? dot(x, DeviceMatrix(ys); return_t) : Array(_fused_interact(dot, x, ys).out)
+    return_t ? dot(x, DeviceMatrix(ys); return_t) :
+    (x isa DeviceMatrix ? _fused_interact(dot, x, ys).out : Array(_fused_interact(dot, x, ys).out))
 (dot::HipDotInteraction)(x::OneDNN.Memory, ys::HipLookup; kw...) = dot(OneDNN.materialize(x), ys; kw...)
 
 function ChainRulesCore.rrule(dot::HipDotInteraction, X, ys::HipLookup{T}) where {T}
@@ -515,7 +518,8 @@ function ChainRulesCore.rrule(dot::HipDotInteraction, X, ys::HipLookup{T}) where
     function dot_pullback(Δ)
         Δh = Δ isa OneDNN.Memory ? OneDNN.materialize(Δ) : Δ
         d, B = size(st.x)
-        st.delta = upload!(DeviceMatrix{T}(st.ctx, size(Δh)...), Matrix{T}(Δh))
+        # a DeviceMatrix Δ (the top MLP on the GPU) is read in place; a host one is uploaded
+        st.delta = Δh isa DeviceMatrix ? Δh : upload!(DeviceMatrix{T}(st.ctx, size(Δh)...), Matrix{T}(Δh))
         if st.ctx.lr !== nothing   # once-hit rows stepped here, the others' dt rows left for update!
             check(st.ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
                                 (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid},
@@ -533,9 +537,9 @@ function ChainRulesCore.rrule(dot::HipDotInteraction, X, ys::HipLookup{T}) where
                                 size(st.dt, 1)))
             st.bwd = :all_dt
         end
-        return (NoTangent(), Array(st.dx), st.dt)
+        return (NoTangent(), Δh isa DeviceMatrix ? st.dx : Array(st.dx), st.dt)
     end
-    return Array(st.out), dot_pullback
+    return (x isa DeviceMatrix ? st.out : Array(st.out)), dot_pullback
 end
 
 function ChainRulesCore.rrule(

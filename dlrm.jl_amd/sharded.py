@@ -40,8 +40,9 @@ All compute goes through a `ShardOps` object: `HipShardOps` (the product: the C-
 or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend "nccl"
 = RCCL over xGMI on MI355X) carries the two all-to-alls (uneven table counts per rank: the
 split-size form of all_to_all_single), or, with exchange="abi", the library's own RCCL
-communicator (dlrm_alltoall_fwd / _bwd, dlrm.jl_amd/comm.py).  The bench replays the compute
-between the two collectives as hipGraphs (`capture`); the collectives are launched eagerly.
+communicator (dlrm_alltoall_fwd / _bwd, dlrm.jl_amd/comm.py).  The bench replays each whole step,
+collectives included, as one hipGraph (`capture_full`); where the backend's collectives cannot be
+captured, the compute between them (`capture`) with the collectives launched eagerly.
 """
 import os
 
@@ -246,6 +247,7 @@ class ShardedHotPath:
         elif exchange != "torch":
             raise ValueError(f"exchange must be 'torch' or 'abi', not {exchange!r}")
         self._graphs = None
+        self._full = None  # capture_full: one graph per index batch, collectives inside
         self._fused_bwd = None  # None: not tried yet; False: the ops cannot (repack instead)
         cuda = dev.type == "cuda"
         self._side = torch.cuda.Stream(device=dev) if cuda else None   # the indexer build
@@ -424,9 +426,32 @@ class ShardedHotPath:
 
     def step_graphed(self, k):
         """One step of index batch k from the captured graphs (same schedule as `step`)."""
+        if self._full is not None:
+            self._full[k].replay()
+            return
         look, mid, upd, ixg = self._graphs
         self._run(None, lambda m: look[k][m].replay(), lambda m: mid[m].replay(), lambda: upd[k].replay(),
                   lambda: ixg[k].replay())
+
+    def capture_full(self, x, idx_list, dout):
+        """One hipGraph per index batch holding the WHOLE step: the side-stream index build, the
+        lookup, both all-to-alls (RCCL: torch.distributed "nccl" or the library's communicator,
+        captured on the step's streams), the interaction and the update -- one replay per step, so
+        M > 1 micro-batch overlap is not launch-bound.  Raises if the backend cannot
+        be captured (gloo); the caller falls back to `capture` (collectives eager)."""
+        if dist.is_initialized() and dist.get_backend(self.group) != "nccl":
+            raise RuntimeError(f"{dist.get_backend(self.group)} collectives cannot be captured")
+        s = torch.cuda.Stream(device=self.out.device)
+        s.wait_stream(torch.cuda.current_stream())
+        graphs = []
+        with torch.cuda.stream(s):
+            for idx in idx_list:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self.step(x, idx, dout)
+                graphs.append(g)
+        torch.cuda.current_stream().wait_stream(s)
+        self._full = graphs
 
 
 def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None, nbatch=8,
@@ -474,12 +499,23 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
     eng.bench_packs = packs  # the index batches (tools/bench_full_step.py drives the full step with them)
 
     def step(k):
-        if eng._graphs is not None:
+        if eng._graphs is not None or eng._full is not None:
             eng.step_graphed(k % nb)
         else:
             eng.step(x, packs[k % nb], dout)
 
-    def prepare_graphs():
+    def prepare_graphs(full=True):
+        """full: the whole step per graph, collectives included (capture_full); else (or if that
+        capture is refused) the compute segments between eager collectives.  Returns the form."""
+        if full:
+            try:
+                eng.capture_full(x, packs, dout)
+                return "full"
+            except Exception as e:  # (a backend whose collectives cannot be captured)
+                eng._full = None
+                import sys
+                print(f"note: whole-step capture refused ({e!r}); graphing the compute segments", file=sys.stderr)
         eng.capture(x, packs, dout)
+        return "segments"
 
     return eng, step, prepare_graphs

@@ -45,10 +45,12 @@ blk = slot // 16
 t0 = st.min()
 names = {1: "chunk", 2: "hot slice", 3: "singles", 4: "next-batch build"}
 print(f"launch: {len(np.unique(blk))} workgroups logged, last item ends at {(en.max() - t0) / 100:.2f} us")
+kslot = slot % 16
 for k in sorted(set(kind.tolist())):
-    m = kind == k
+  for ks in ([0, 1] if k == 4 and (kslot[kind == 4] == 1).any() else [None]):
+    m = (kind == k) if ks is None else ((kind == k) & (kslot == ks))
     d = (en[m] - st[m]) / 100
-    print(f"{names.get(k, k):17s} items {m.sum():5d}  start {(st[m].min() - t0) / 100:6.2f}..{(st[m].max() - t0) / 100:6.2f}"
+    print(f"{names.get(k, k) + ('' if ks is None else f' #{ks}'):17s} items {m.sum():5d}  start {(st[m].min() - t0) / 100:6.2f}..{(st[m].max() - t0) / 100:6.2f}"
           f"  end p50 {np.percentile((en[m] - t0) / 100, 50):6.2f} max {(en[m].max() - t0) / 100:6.2f}"
           f"  dur p50/p90/max {np.percentile(d, 50):.2f}/{np.percentile(d, 90):.2f}/{d.max():.2f} us")
 # items per workgroup (apply blocks only)
@@ -85,3 +87,19 @@ if ok.any():
             print(f"  mark {k:2d}: {np.percentile(r, 50):6.2f} / {r.max():6.2f}")
     end = (en[kind == 4].max() - t0) / 100
     print("  (build item durations above include the marks' own barriers)")
+
+# wave build marks (g_wph[block][wave][k]): 0 start, 1 indices loaded + counted, 2 compacted,
+# 3 first counting pass, 4 sorted, 5 segments written, 6 chunks / slices written
+if hasattr(lib, "dlrm_debug_wph"):
+    wb = (ctypes.c_ulonglong * (256 * 4 * 16))()
+    lib.dlrm_debug_wph(wb)
+    a3 = np.array(wb, dtype=np.int64).reshape(256, 4, 16)[:int((kind == 4).sum())].reshape(-1, 16)
+    ok = a3[:, 0] > 0
+    if ok.any():
+        rel = (a3[ok] - a3[ok][:, :1]) / 100
+        print("wave build marks over", int(ok.sum()), "waves (us from the wave's mark 0: p50 / max):")
+        for k in range(1, 16):
+            col = a3[ok][:, k]
+            if (col > 0).any():
+                r = rel[:, k][col > 0]
+                print(f"  mark {k:2d}: {np.percentile(r, 50):6.2f} / {r.max():6.2f}")
