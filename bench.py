@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
                          "0: the engine's default (1: DESIGN.md §6)")
-    ap.add_argument("--shard-graph", choices=["full", "segments"], default="full",
+    ap.add_argument("--shard-graph", choices=["full", "segments"], default="segments",
                     help="multi-GPU graph form: 'full' = one hipGraph per step with the RCCL all-to-alls "
                          "inside (falls back to 'segments' where the capture is refused); 'segments' = the "
                          "compute between eager collectives")

@@ -651,6 +651,29 @@ int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables*
     return DLRM_OK;
 }
 
+int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, const void* indices, int itype,
+                         int64_t table_stride, int index_base, int batch) {
+    CHECK_ARG(ctx && ix && tb, "dlrm_indexer_prepare: null argument");
+    int rc = check_indices(ctx, tb, indices, itype, table_stride, batch, 1);
+    if (rc) return rc;
+    CHECK_ARG(tb->T == ix->T, "dlrm_indexer_prepare: indexer has %d tables, tables has %d", ix->T, tb->T);
+    CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_prepare: batch %d > capacity %lld", batch, (long long)ix->dev.cap);
+    if (batch > kStepIndexMaxN || tb->T + 1 > 32 || ix->TV != kStepMaxParts * ix->T)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d, %d tables (the step build: batch <= %d, "
+                        "<= 31 tables)", batch, tb->T, kStepIndexMaxN);
+    ix->built = false;
+    ix->prepared = false;
+    ix->dev.vshift = step_parts_log2(kWaveBuildParts);
+    if (ix->dev.vshift < 2) ix->dev.vshift = 2;
+    rc = launch_step_prepare(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
+                             ix->prep_err);
+    if (rc) return rc;
+    record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+    ix->prepared = true;
+    ix->dev.has_map = 1;
+    return DLRM_OK;
+}
+
 // One (virtual) table's build, whole: rows, grouped positions, segment starts.
 struct IndexerTable {
     std::vector<uint32_t> rows;

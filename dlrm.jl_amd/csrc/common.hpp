@@ -340,6 +340,8 @@ int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const voi
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
                          int itype, int64_t tstride, int base, int B, int L, bool split = false,
                          hipStream_t stream = nullptr);
+int launch_step_prepare(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
+                        int64_t tstride, int base, int N, unsigned* err);
 struct SinglesArgs;
 struct PrepArgs;
 int launch_sgd_apply(dlrm_ctx* ctx, const IndexerDev& ix, TableDesc* tabs, bool tabs_aligned16, int T, int D,

@@ -607,25 +607,23 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
 
 
 // ------------------------------------------------------------- wave build (round 4)
-// The training step's split build of the NEXT batch, by ONE WAVE per virtual table (t, part):
-// no workgroup barrier after the first.  The 256-thread block build (fast_index_table) took
-// ~12 us per part inside the apply launch: ~15 dependent barrier + LDS phases with one wave per
-// SIMD, its length the same alone, beside the apply, or run twice on a warm instruction cache
-// (tools/phase_step.py, profiles/r10_apply_timeline.txt).  Here a workgroup's 4 waves take 4
-// consecutive parts of one table -- their keys together are at most the table's N positions,
-// so one pool sized for N holds them, each wave taking its share by an LDS cursor -- and each
-// wave sorts ~N/16 keys with wave-level steps only.
+// The training step's split build of the NEXT batch, one WAVE per virtual table (t, part).  The
+// 256-thread block build (fast_index_table) took ~12 us per part inside the apply launch: ~15
+// dependent barrier + LDS phases with one wave per SIMD, the same alone, beside the apply, or
+// run twice on a warm instruction cache (tools/phase_step.py).  Here a workgroup of 4 waves
+// splits one table's positions among 4 parts together (each wave reads a quarter of them once),
+// then each wave sorts its part (~N/16 keys at 16 parts per table) with wave-level steps: DPP
+// scans, ballots, one LDS atomic per digit group, and no workgroup barrier.
 // Output format = fast_index_table's (split): the apply, dlrm_indexer_read and the step backward
 // read it unchanged.  Within a part, segments come in ascending row order, positions ascending.
 constexpr int kWaveParts = 4;       // waves per build workgroup = parts of one table per workgroup
 constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-byte bucket is this small
-constexpr int kApplyMapThreads = kWaveParts * 64;  // the workgroup that writes the item map
 struct WaveBuildLds {
-    uint32_t K[2][kStepIndexMaxN];  // keys (row >> vshift), sort ping-pong; pool shared by the 4 waves
+    uint32_t K[2][kStepIndexMaxN];  // keys (row >> vshift), sort ping-pong; the 4 parts' regions
     int32_t V[2][kStepIndexMaxN];   // positions
     int32_t R[kStepIndexMaxN];      // per-key rank in its digit, then segment starts
     uint32_t cnt[kWaveParts][256];  // per-wave digit counters, then digit offsets
-    int cursor;                     // pool allocation
+    int tot[kWaveParts][kWaveParts];  // [wave][part]: positions of the workgroup's part q that wave w read
 };
 
 __device__ __forceinline__ unsigned long long lanes_below() {
@@ -714,97 +712,35 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
     wave_lds_sync();
 }
 
-// Virtual table v = (t << vs) + part of the split build, by the calling wave (w = its index in
-// the workgroup); sl.cursor was zeroed before a workgroup barrier.  Lane l reads positions
-// [32 l, 32 l + 32) of the table (one contiguous 128-B run: 16-B loads), so the part's keys are
-// compacted in position order by one wave scan of the lanes' counts, with no per-tile ballot.
-__device__ void wave_index_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows,
-                                const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
-                                unsigned* __restrict__ err, WaveBuildLds& sl, int w) {
+// The last build workgroup: the flat lists' totals (every wave's reservation add returned before
+// its workgroup arrived), then the counters reset for this indexer's next build (a later launch).
+__device__ void finish_item_lists(const IndexerDev& ix) {
+    if (threadIdx.x == 0) {
+        const unsigned c = __hip_atomic_load(ix.build_arrive + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned s = __hip_atomic_load(ix.build_arrive + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ix.item_tot[0] = (int)s;
+        ix.item_tot[1] = (int)c;
+        ix.build_arrive[0] = 0u;
+        ix.build_arrive[1] = 0u;
+        ix.build_arrive[2] = 0u;
+    }
+}
+
+// The part the calling wave sorts and writes out: virtual table v = (t << vs) + part, its n keys
+// (row >> vs) and positions in position order at K0 / V0 (K1, V1, R: the same span of the pool's
+// other arrays, scratch).  Sorts them in LDS (one counting pass on the low 8 key bits, then a
+// within-bucket rank or, for skewed rows, the remaining LSD passes), classifies the segments
+// (LDS only), reserves the wave's range of the flat item lists (one atomic add per kind: before
+// any store of this wave, so its wait covers no store), arrives with the workgroup, and only then
+// stores every output.
+__device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
+                               int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, WaveBuildLds& sl,
+                               int groups) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lanes_below();
-    const uint32_t pmask = (1u << vs) - 1u, part = (uint32_t)v & pmask;
+    const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
     const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
     const int nbits = 32 - __clz(kmax);
-    constexpr int E = kStepIndexMaxN / 64;  // positions per lane
-    constexpr int KB = E / 4;               // 16-B pieces per lane: piece k covers positions
-                                            // [256 k + 4 lane, +4) (wave-coalesced, 1 KB per load)
-    WPH(0);
-    // the lane's E indices: 16-B loads when whole and aligned, else one by one; each validated
-    // (0 <= row < nrows; out of range raises BoundsError, part 0 reports it) and kept when it is
-    // this part's.  Element j = 4 k + e is position 256 k + 4 lane + e.
-    uint32_t rv[E];       // row (32-bit)
-    uint32_t keep = 0;    // bit j: element j is this part's
-    bool bad = false;
-    {
-        const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
-        const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
-        const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
-        if (vec && itype == DLRM_I32) {
-            int4 q[KB];
-#pragma unroll
-            for (int k = 0; k < KB; ++k)
-                if (256 * k < N) q[k] = ldg<int4>(i32 + 256 * k + 4 * lane);  // (uniform guard)
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                if (256 * k >= N) break;
-                const int32_t e4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t r = (int64_t)e4[e] - base;
-                    const bool ok = (uint64_t)r < (uint64_t)nrows;  // (negative: a huge unsigned)
-                    bad |= !ok;
-                    keep |= (ok && ((uint32_t)r & pmask) == part) ? (1u << (4 * k + e)) : 0u;
-                    rv[4 * k + e] = (uint32_t)r;
-                }
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < E; ++j) {
-                const int pj = 256 * (j >> 2) + 4 * lane + (j & 3);
-                const bool in = pj < N;
-                const int64_t r = load_index_if(in, idx, itype, (int64_t)t * tstride + pj) - base;
-                const bool ok = in && r >= 0 && r < (int64_t)nrows;
-                bad |= in && !ok;
-                keep |= (ok && ((uint32_t)r & pmask) == part) ? (1u << j) : 0u;
-                rv[j] = (uint32_t)r;
-            }
-        }
-    }
-    if (part == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
-    // compaction in position order (piece k of every lane before piece k + 1): per piece a DPP
-    // scan of the lanes' kept counts
-    int kbase[KB];
-    int n = 0;
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-        const int c = __popc((keep >> (4 * k)) & 0xfu);
-        const int incl = wave_incl_scan(c);
-        kbase[k] = n + incl - c;
-        n += lane63(incl);
-    }
-    WPH(1);
-    int pb = 0;
-    if (lane == 0) pb = atomicAdd(&sl.cursor, n);
-    pb = __builtin_amdgcn_readfirstlane(pb);
-    uint32_t* K0 = sl.K[0] + pb;
-    uint32_t* K1 = sl.K[1] + pb;
-    int32_t* V0 = sl.V[0] + pb;
-    int32_t* V1 = sl.V[1] + pb;
-    int32_t* R = sl.R + pb;
-    uint32_t* cnt = sl.cnt[w];
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-        int q = kbase[k];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if ((keep >> (4 * k + e)) & 1u) {
-                K0[q] = rv[4 * k + e] >> vs;
-                V0[q] = 256 * k + 4 * lane + e;
-                ++q;
-            }
-    }
-    wave_lds_sync();
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
@@ -830,44 +766,58 @@ __device__ void wave_index_part(const IndexerDev& ix, int v, int t, int vs, uint
         }
     }
     WPH(4);
-    // segments: perm, seg_start / seg_row, once-hit flags; segment starts kept in R
+    // segment starts (R[s]) and counts, LDS only
+    int U = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int i = j0 + lane;
+        const bool head = i < n && (i == 0 || Ks[i - 1] != Ks[i]);
+        const unsigned long long hb = __ballot(head);
+        if (head) R[U + __popcll(hb & lt)] = i;
+        U += __popcll(hb);
+    }
+    wave_lds_sync();
+    int C = 0, S = 0;
+    for (int s0 = 0; s0 < U; s0 += 64) {
+        const int s = s0 + lane;
+        const int len = s < U ? (s + 1 < U ? R[s + 1] : n) - R[s] : 0;
+        C += __popcll(__ballot(len >= 2 && len <= kChunk));
+        S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
+    }
+    unsigned cbase = 0, sbase = 0;
+    if (lane == 0) {
+        if (C) cbase = __hip_atomic_fetch_add(ix.build_arrive + 1, (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (S) sbase = __hip_atomic_fetch_add(ix.build_arrive + 2, (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    cbase = __builtin_amdgcn_readfirstlane(cbase);
+    sbase = __builtin_amdgcn_readfirstlane(sbase);
+    // every wave of the workgroup has reserved: one arrival for the workgroup (the last one
+    // publishes the lists' totals and resets the counters; the stores below are read in a later launch)
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(ix.build_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(groups - 1))
+        finish_item_lists(ix);
+    WPH(5);
+    // the outputs: perm, once-hit flags, segments, per-table chunk / hot lists, counts, flat records
     const int64_t off = (int64_t)v * ix.cap;
     int32_t* perm = ix.perm + off;
     int32_t* seg_start = ix.seg_start + (int64_t)v * (ix.cap + 1);
     uint32_t* seg_row = ix.seg_row + off;
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
-    int U = 0;
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int i = j0 + lane;
-        const bool ok = i < n;
-        const uint32_t k = ok ? Ks[i] : 0u;
-        const bool head = ok && (i == 0 || Ks[i - 1] != k);
-        const bool tail = ok && (i + 1 == n || Ks[i + 1] != k);
-        if (ok) {
+        if (i < n) {
+            const uint32_t k = Ks[i];
+            const bool head = i == 0 || Ks[i - 1] != k;
+            const bool tail = i + 1 == n || Ks[i + 1] != k;
             const int p = Vs[i];
             perm[i] = p;
             single[p] = (head && tail) ? 1 : 0;
         }
-        const unsigned long long hb = __ballot(head);
-        if (head) {
-            const int s = U + __popcll(hb & lt);
-            seg_start[s] = i;
-            seg_row[s] = (k << vs) | part;
-            R[s] = i;
-        }
-        U += __popcll(hb);
     }
-    if (lane == 0) seg_start[U] = n;
-    wave_lds_sync();
-    WPH(5);
-    // chunks (2 ..kChunk positions; once-hit positions are the backward's), hot segments + slices:
-    // per virtual table (dlrm_indexer_read, the counts-scanning apply), then, with this wave's
-    // range of the flat lists reserved by one atomic add per kind, as flat records (the
-    // item-map apply: one load per item)
     int4* chunks = ix.chunks + 2 * off;
     int4* hot = ix.hot + off;
     int4* hot_slice = ix.hot_slice + off;
-    int C = 0, H = 0, S = 0;
+    int c = 0, h = 0, sl0 = 0;
     for (int s0 = 0; s0 < U; s0 += 64) {
         const int s = s0 + lane;
         const bool ok = s < U;
@@ -880,91 +830,174 @@ __device__ void wave_index_part(const IndexerDev& ix, int v, int t, int vs, uint
         const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
         const int sincl = wave_incl_scan(ns);
         const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
-        if (isc) write_chunk(chunks, C + __popcll(cb & lt), beg, end, row, Vs);
-        if (ish) {
-            const int h = H + __popcll(hb & lt), s0s = S + sincl - ns;
-            hot[h] = make_int4(beg, end, row, s0s);
-            write_slices(hot_slice, s0s, beg, end, row, h);
+        if (ok) {
+            seg_start[s] = beg;
+            seg_row[s] = (uint32_t)row;
         }
-        C += __popcll(cb);
-        H += __popcll(hb);
-        S += lane63(sincl);
+        if (isc) {
+            const int ci = c + __popcll(cb & lt);
+            write_chunk(chunks, ci, beg, end, row, Vs);
+            write_chunk_rec(ix.chunk_rec, (int64_t)cbase + ci, (int)(off + beg), (int)(off + end), row, Vs + beg);
+        }
+        if (ish) {
+            const int hi = h + __popcll(hb & lt), sloc = sl0 + sincl - ns, first = (int)sbase + sloc;
+            hot[hi] = make_int4(beg, end, row, sloc);
+            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
+                const int p1 = min(p0 + kHotSlice, end);
+                hot_slice[sloc + k] = make_int4(p0, p1, row, hi);
+                ix.slice_rec[2 * (int64_t)(first + k)] = make_int4((int)(off + p0), (int)(off + p1), row, v);
+                ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
+            }
+        }
+        c += __popcll(cb);
+        h += __popcll(hb);
+        sl0 += lane63(sincl);
     }
     if (lane == 0) {
+        seg_start[U] = n;
         int32_t* cn = ix.counts + (int64_t)v * 8;
-        cn[CNT_U] = U; cn[CNT_C] = C; cn[CNT_H] = H; cn[CNT_S] = S; cn[CNT_NV] = n;
-    }
-    if (C + S > 0) {
-        unsigned cbase = 0, sbase = 0;
-        if (lane == 0) {
-            if (C) cbase = __hip_atomic_fetch_add(ix.build_arrive + 1, (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (S) sbase = __hip_atomic_fetch_add(ix.build_arrive + 2, (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        cbase = __builtin_amdgcn_readfirstlane(cbase);
-        sbase = __builtin_amdgcn_readfirstlane(sbase);
-        int c = 0, sl = 0;
-        for (int s0 = 0; s0 < U; s0 += 64) {
-            const int s = s0 + lane;
-            const bool ok = s < U;
-            const int beg = ok ? R[s] : 0;
-            const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
-            const int len = end - beg;
-            const bool isc = ok && len >= 2 && len <= kChunk;
-            const bool ish = ok && len > kChunk;
-            const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
-            const unsigned long long cb = __ballot(isc);
-            const int sincl = wave_incl_scan(ns);
-            const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
-            if (isc) {  // the descriptor with global perm entries (v * cap + local)
-                const int64_t f = (int64_t)cbase + c + __popcll(cb & lt);
-                write_chunk_rec(ix.chunk_rec, f, (int)(off + beg), (int)(off + end), row, Vs + beg);
-            }
-            if (ish) {
-                const int first = (int)sbase + sl + sincl - ns;
-                for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
-                    ix.slice_rec[2 * (int64_t)(first + k)] =
-                        make_int4((int)(off + p0), (int)(off + min(p0 + kHotSlice, end)), row, v);
-                    ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
-                }
-            }
-            c += __popcll(cb);
-            sl += lane63(sincl);
-        }
+        cn[CNT_U] = U; cn[CNT_C] = c; cn[CNT_H] = h; cn[CNT_S] = sl0; cn[CNT_NV] = n;
     }
     WPH(6);
 }
 
-// The last build workgroup: the flat lists' totals (every wave's reservation add returned before
-// its workgroup arrived), then the counters reset for this indexer's next build (a later launch).
-__device__ void finish_item_lists(const IndexerDev& ix) {
-    if (threadIdx.x == 0) {
-        const unsigned c = __hip_atomic_load(ix.build_arrive + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned s = __hip_atomic_load(ix.build_arrive + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ix.item_tot[0] = (int)s;
-        ix.item_tot[1] = (int)c;
-        ix.build_arrive[0] = 0u;
-        ix.build_arrive[1] = 0u;
-        ix.build_arrive[2] = 0u;
-    }
-}
-
-// One build workgroup (kWaveParts waves = 256 threads): parts g*4 .. g*4+3 of table (g*4) >> vs
-// (vs >= 2) of T tables.  Every thread of the workgroup calls it.  The last of the T << vs >> 2
-// workgroups to arrive (one agent-scope add per workgroup, after its waves' reservation adds have
-// returned) publishes the flat lists' totals (finish_item_lists).
+// One build workgroup (kWaveParts waves = 256 threads): parts q0 .. q0 + 3 (q0 = 4 (g mod P / 4))
+// of table t = g / (P / 4), P = 2^vs >= 4 parts per table.  Every thread of the workgroup calls
+// it.  The four waves first split the table's positions among the four parts together -- wave w
+// reads positions [512 w, 512 w + 512), 16-B loads, and the parts' lists keep position order by
+// (wave, piece, lane) offsets from DPP scans and one exchange of per-wave counts -- then wave q
+// sorts part q0 + q alone (wave_sort_part).  The last of the T P / 4 workgroups to arrive
+// publishes the flat lists' totals (finish_item_lists).
 __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
                                  const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
                                  unsigned* __restrict__ err, WaveBuildLds& sl) {
-    if (threadIdx.x == 0) sl.cursor = 0;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
+    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const uint32_t pmask = (1u << vs) - 1u;
+    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
+    constexpr int WS = kStepIndexMaxN / kWaveParts;  // positions per wave
+    constexpr int PK = WS / 256;                     // 16-B pieces per lane
+    WPH(0);
+    // element j = 4 k + e: position WS w + 256 k + 4 lane + e; code = its part - q0 (0..3), or 4
+    uint32_t rv[4 * PK];
+    uint32_t code = 0;  // 3 bits per element
+    bool bad = false;
+    {
+        const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+        const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
+        const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
+        int64_t r[4 * PK];
+        bool in[4 * PK];
+        if (vec && itype == DLRM_I32) {
+            int4 q[PK];
+#pragma unroll
+            for (int k = 0; k < PK; ++k)
+                if (WS * w + 256 * k < N) q[k] = ldg<int4>(i32 + WS * w + 256 * k + 4 * lane);
+#pragma unroll
+            for (int k = 0; k < PK; ++k) {
+                const bool kin = WS * w + 256 * k < N;
+                r[4 * k] = q[k].x; r[4 * k + 1] = q[k].y; r[4 * k + 2] = q[k].z; r[4 * k + 3] = q[k].w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) in[4 * k + e] = kin;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4 * PK; ++j) {
+                const int pj = WS * w + 256 * (j >> 2) + 4 * lane + (j & 3);
+                in[j] = pj < N;
+                r[j] = load_index_if(in[j], idx, itype, (int64_t)t * tstride + pj);
+            }
+        }
+        WPH(7);
+#pragma unroll
+        for (int j = 0; j < 4 * PK; ++j) {
+            const int64_t rr = r[j] - base;
+            const bool ok = in[j] && (uint64_t)rr < (uint64_t)nrows;  // (negative: a huge unsigned)
+            bad |= in[j] && !ok;
+            const uint32_t pq = ((uint32_t)rr & pmask) - (uint32_t)q0;
+            code |= (ok && pq < (uint32_t)kWaveParts ? pq : 4u) << (3 * j);
+            rv[j] = (uint32_t)rr >> vs;
+        }
+    }
+    // out of range raises BoundsError; the workgroup of parts 0..3 reports it
+    if (q0 == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    // per piece k and part q: this lane's count, a DPP scan over the lanes (two 16-bit fields per word)
+    int pre[PK][kWaveParts], ptot[PK][kWaveParts];
+#pragma unroll
+    for (int k = 0; k < PK; ++k) {
+        int cq[kWaveParts] = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t cd = (code >> (3 * (4 * k + e))) & 7u;
+#pragma unroll
+            for (int q = 0; q < kWaveParts; ++q) cq[q] += cd == (uint32_t)q ? 1 : 0;
+        }
+        const int a = cq[0] | (cq[1] << 16), b = cq[2] | (cq[3] << 16);
+        const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+        const int ta = lane63(ia), tb = lane63(ib);
+        pre[k][0] = (ia - a) & 0xffff; pre[k][1] = (ia - a) >> 16;
+        pre[k][2] = (ib - b) & 0xffff; pre[k][3] = (ib - b) >> 16;
+        ptot[k][0] = ta & 0xffff; ptot[k][1] = ta >> 16; ptot[k][2] = tb & 0xffff; ptot[k][3] = tb >> 16;
+    }
+    if (lane < kWaveParts) {
+        int tw = 0;
+#pragma unroll
+        for (int k = 0; k < PK; ++k)
+#pragma unroll
+            for (int q = 0; q < kWaveParts; ++q) tw += lane == q ? ptot[k][q] : 0;
+        sl.tot[w][lane] = tw;
+    }
     __syncthreads();
-    const int w = threadIdx.x >> 6;
-    const int v = g * kWaveParts + w, t = v >> ix.vshift;
-    wave_index_part(ix, v, t, ix.vshift, (uint32_t)load_table(tabs, t).nrows, idx, itype, tstride, base, N, err, sl, w);
-    const int groups = (T << ix.vshift) / kWaveParts;
+    // part q's region of the pool, and this wave's offset in it
+    int pbase[kWaveParts], woff[kWaveParts], n_of[kWaveParts];
+    {
+        int run = 0;
+#pragma unroll
+        for (int q = 0; q < kWaveParts; ++q) {
+            int nq = 0, wq = 0;
+#pragma unroll
+            for (int ww = 0; ww < kWaveParts; ++ww) {
+                const int c = sl.tot[ww][q];
+                nq += c;
+                wq += ww < w ? c : 0;
+            }
+            pbase[q] = run;
+            woff[q] = wq;
+            n_of[q] = nq;
+            run += nq;
+        }
+    }
+    WPH(1);
+#pragma unroll
+    for (int k = 0; k < PK; ++k) {
+        int at[kWaveParts];
+#pragma unroll
+        for (int q = 0; q < kWaveParts; ++q) {
+            int before = 0;
+#pragma unroll
+            for (int kk = 0; kk < k; ++kk) before += ptot[kk][q];
+            at[q] = pbase[q] + woff[q] + before + pre[k][q];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t cd = (code >> (3 * (4 * k + e))) & 7u;
+            if (cd < (uint32_t)kWaveParts) {
+                int dst = 0;
+#pragma unroll
+                for (int q = 0; q < kWaveParts; ++q)
+                    if (cd == (uint32_t)q) dst = at[q]++;
+                sl.K[0][dst] = rv[4 * k + e];
+                sl.V[0][dst] = WS * w + 256 * k + 4 * lane + e;
+            }
+        }
+    }
     __syncthreads();
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(ix.build_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(groups - 1))
-        finish_item_lists(ix);
+    // wave w sorts part q0 + w
+    const int pb = pbase[w], n = n_of[w];
+    const int v = (t << vs) + q0 + w;
+    wave_sort_part(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
+                   sl.cnt[w], sl, (T << vs) / kWaveParts);
 }
 
 }  // namespace dlrm

@@ -518,6 +518,16 @@ static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
                        sizeof(WaveBuildLds), s, pa);
 }
 
+// The step's split build alone (dlrm_indexer_prepare): the wave build + item lists, 4 parts per
+// workgroup, on the ctx's stream (a caller's side stream: it depends on the indices only).
+int launch_step_prepare(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx, int itype,
+                        int64_t tstride, int base, int N, unsigned* err) {
+    if (T_ == 0 || N == 0) return DLRM_OK;
+    const PrepArgs pa{ix, tabs, T_, idx, itype, tstride, base, N, err};
+    launch_step_index(ctx_stream(ctx), pa);
+    return ctx_hip(ctx, hipGetLastError(), "step_index launch");
+}
+
 // Generic (any D) versions: one thread per element column.
 template <typename TT, typename GT>
 __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,

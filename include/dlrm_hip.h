@@ -227,6 +227,14 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
                       int64_t* num_unique, int64_t* rows, int64_t* positions,
                       int64_t* seg_start, int64_t cap);
 
+/* The training step's split build of `indices` on the ctx's stream -- a side stream: it depends on
+ * the indices only -- so that the dlrm_step_fwd of the same indices only gathers (the build
+ * dlrm_step_bwd_prepare runs inside an apply launch, as its own launch).  batch <= 2048, <= 31
+ * tables.  Replaces the SparseIndexer() build of train.jl:276-281 ahead of the step.  Bounds errors
+ * are raised by that forward. */
+int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
+                         const void* indices, int itype, int64_t table_stride, int index_base, int batch);
+
 /* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
  * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only
  * the repeated rows' gradients.  (The Julia shim's pullback state, DLRMHip.jl `st.bwd`.) */

@@ -88,8 +88,9 @@ if ok.any():
     end = (en[kind == 4].max() - t0) / 100
     print("  (build item durations above include the marks' own barriers)")
 
-# wave build marks (g_wph[block][wave][k]): 0 start, 1 indices loaded + counted, 2 compacted,
-# 3 first counting pass, 4 sorted, 5 segments written, 6 chunks / slices written
+# wave build marks (g_wph[block][wave][k]): 0 start, 7 index loads issued, 8 landed, 9 validated,
+# 1 counted (scans), 2 compacted, 3 first counting pass, 4 sorted, 5 segments written, 6 chunks /
+# slices written
 if hasattr(lib, "dlrm_debug_wph"):
     wb = (ctypes.c_ulonglong * (256 * 4 * 16))()
     lib.dlrm_debug_wph(wb)
