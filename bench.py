@@ -35,8 +35,8 @@ CHUNK = 64  # steps per captured hipGraph
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=640)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--workload", default="kaggle-d128-b2048")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: the global batch (split evenly over the ranks; e.g. configs[3]: "

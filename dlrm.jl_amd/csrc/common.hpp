@@ -244,16 +244,16 @@ struct IndexerDev {
     int vshift;
     int hbits;
     // flat item lists of the wave build (apply.hpp reads them when has_map): every build wave
-    // reserves its hot slices and chunks with one atomic add per kind on build_arrive[2] / [1] and
-    // writes them whole; the last build workgroup (build_arrive[0] counts them in) copies the
-    // totals to item_tot = {hot slices, chunks} and resets the three counters.
+    // reserves its hot slices and chunks and arrives with ONE 64-bit atomic add on build_arrive
+    // (indexer.hpp kRes*Shift packing) and writes them whole; the last wave to arrive copies the
+    // totals to item_tot = {hot slices, chunks} and clears the word.
     //   slice_rec[2k, 2k+1]: {first perm entry, end (global: v * cap + local), row, v},
     //                        {slices of its segment, flat index of the segment's first slice, 0, 0}
     //   chunk_rec[2c, 2c+1]: the chunk descriptor (write_chunk) with global perm entries
     int4* slice_rec;
     int4* chunk_rec;
     int32_t* item_tot;
-    uint32_t* build_arrive;  // [0] build workgroups arrived, [1] chunks, [2] hot slices reserved
+    uint32_t* build_arrive;  // the reservation word (64 bits, 8-B aligned)
     int has_map;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)

@@ -626,6 +626,10 @@ struct WaveBuildLds {
     int tot[kWaveParts][kWaveParts];  // [wave][part]: positions of the workgroup's part q that wave w read
 };
 
+// The flat item lists' reservation word (build_arrive, 64 bits): chunks in bits 0..23, hot slices
+// in 24..43, arrived build waves in 44..63 (the wave build: <= 31 x 2048 positions).
+constexpr int kResSliceShift = 24, kResArriveShift = 44;
+
 __device__ __forceinline__ unsigned long long lanes_below() {
     const int lane = threadIdx.x & 63;
     return lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -712,27 +716,12 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
     wave_lds_sync();
 }
 
-// The last build workgroup: the flat lists' totals (every wave's reservation add returned before
-// its workgroup arrived), then the counters reset for this indexer's next build (a later launch).
-__device__ void finish_item_lists(const IndexerDev& ix) {
-    if (threadIdx.x == 0) {
-        const unsigned c = __hip_atomic_load(ix.build_arrive + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned s = __hip_atomic_load(ix.build_arrive + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ix.item_tot[0] = (int)s;
-        ix.item_tot[1] = (int)c;
-        ix.build_arrive[0] = 0u;
-        ix.build_arrive[1] = 0u;
-        ix.build_arrive[2] = 0u;
-    }
-}
-
 // The part the calling wave sorts and writes out: virtual table v = (t << vs) + part, its n keys
 // (row >> vs) and positions in position order at K0 / V0 (K1, V1, R: the same span of the pool's
 // other arrays, scratch).  Sorts them in LDS (one counting pass on the low 8 key bits, then a
 // within-bucket rank or, for skewed rows, the remaining LSD passes), classifies the segments
-// (LDS only), reserves the wave's range of the flat item lists (one atomic add per kind: before
-// any store of this wave, so its wait covers no store), arrives with the workgroup, and only then
-// stores every output.
+// (LDS only), reserves the wave's ranges of the flat item lists and arrives in one packed atomic
+// add, stores the per-table outputs while it is in flight, then the flat records at its return.
 __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
                                int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, WaveBuildLds& sl,
                                int groups) {
@@ -783,21 +772,22 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
         C += __popcll(__ballot(len >= 2 && len <= kChunk));
         S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
     }
-    unsigned cbase = 0, sbase = 0;
+    // The wave reserves its flat-list ranges and arrives in ONE atomic add (lane 0), issued before
+    // any store: the stores below run while it is in flight, and only the flat records wait for it.
+    unsigned long long res = 0ull;
+    unsigned long long* word = (unsigned long long*)ix.build_arrive;
     if (lane == 0) {
-        if (C) cbase = __hip_atomic_fetch_add(ix.build_arrive + 1, (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (S) sbase = __hip_atomic_fetch_add(ix.build_arrive + 2, (unsigned)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (a zero the compiler cannot see through: a uniform address gets the wave-aggregating
+        // atomic rewrite, whose readfirstlane would wait for the return right here)
+        int zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        res = __hip_atomic_fetch_add(word + zero,
+                                     (unsigned long long)C + ((unsigned long long)S << kResSliceShift) +
+                                         (1ull << kResArriveShift),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    cbase = __builtin_amdgcn_readfirstlane(cbase);
-    sbase = __builtin_amdgcn_readfirstlane(sbase);
-    // every wave of the workgroup has reserved: one arrival for the workgroup (the last one
-    // publishes the lists' totals and resets the counters; the stores below are read in a later launch)
-    __syncthreads();
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(ix.build_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(groups - 1))
-        finish_item_lists(ix);
     WPH(5);
-    // the outputs: perm, once-hit flags, segments, per-table chunk / hot lists, counts, flat records
+    // the outputs: perm, once-hit flags, segments, per-table chunk / hot lists, counts
     const int64_t off = (int64_t)v * ix.cap;
     int32_t* perm = ix.perm + off;
     int32_t* seg_start = ix.seg_start + (int64_t)v * (ix.cap + 1);
@@ -834,20 +824,12 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
             seg_start[s] = beg;
             seg_row[s] = (uint32_t)row;
         }
-        if (isc) {
-            const int ci = c + __popcll(cb & lt);
-            write_chunk(chunks, ci, beg, end, row, Vs);
-            write_chunk_rec(ix.chunk_rec, (int64_t)cbase + ci, (int)(off + beg), (int)(off + end), row, Vs + beg);
-        }
+        if (isc) write_chunk(chunks, c + __popcll(cb & lt), beg, end, row, Vs);
         if (ish) {
-            const int hi = h + __popcll(hb & lt), sloc = sl0 + sincl - ns, first = (int)sbase + sloc;
+            const int hi = h + __popcll(hb & lt), sloc = sl0 + sincl - ns;
             hot[hi] = make_int4(beg, end, row, sloc);
-            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
-                const int p1 = min(p0 + kHotSlice, end);
-                hot_slice[sloc + k] = make_int4(p0, p1, row, hi);
-                ix.slice_rec[2 * (int64_t)(first + k)] = make_int4((int)(off + p0), (int)(off + p1), row, v);
-                ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
-            }
+            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice)
+                hot_slice[sloc + k] = make_int4(p0, min(p0 + kHotSlice, end), row, hi);
         }
         c += __popcll(cb);
         h += __popcll(hb);
@@ -857,6 +839,46 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
         seg_start[U] = n;
         int32_t* cn = ix.counts + (int64_t)v * 8;
         cn[CNT_U] = U; cn[CNT_C] = c; cn[CNT_H] = h; cn[CNT_S] = sl0; cn[CNT_NV] = n;
+    }
+    // the reservation's return: the wave's bases; the last of the groups x kWaveParts waves to
+    // arrive publishes the lists' totals and clears the word for this indexer's next build (read
+    // in a later launch)
+    res = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(res >> 32)) << 32) |
+          (unsigned)__builtin_amdgcn_readfirstlane((unsigned)res);
+    const int cbase = (int)(res & ((1u << kResSliceShift) - 1u));
+    const int sbase = (int)((res >> kResSliceShift) & ((1u << (kResArriveShift - kResSliceShift)) - 1u));
+    if (lane == 0 && (unsigned)(res >> kResArriveShift) == (unsigned)(groups * kWaveParts - 1)) {
+        ix.item_tot[0] = sbase + S;
+        ix.item_tot[1] = cbase + C;
+        *word = 0ull;
+    }
+    // the flat records (chunk_rec, slice_rec) at the reserved ranges
+    c = 0;
+    sl0 = 0;
+    for (int s0 = 0; s0 < U; s0 += 64) {
+        const int s = s0 + lane;
+        const bool ok = s < U;
+        const int beg = ok ? R[s] : 0;
+        const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
+        const int len = end - beg;
+        const bool isc = ok && len >= 2 && len <= kChunk;
+        const bool ish = ok && len > kChunk;
+        const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
+        const unsigned long long cb = __ballot(isc);
+        const int sincl = wave_incl_scan(ns);
+        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
+        if (isc)
+            write_chunk_rec(ix.chunk_rec, (int64_t)cbase + c + __popcll(cb & lt), (int)(off + beg), (int)(off + end),
+                            row, Vs + beg);
+        if (ish) {
+            const int first = sbase + sl0 + sincl - ns;
+            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
+                ix.slice_rec[2 * (int64_t)(first + k)] = make_int4((int)(off + p0), (int)(off + min(p0 + kHotSlice, end)), row, v);
+                ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
+            }
+        }
+        c += __popcll(cb);
+        sl0 += lane63(sincl);
     }
     WPH(6);
 }
