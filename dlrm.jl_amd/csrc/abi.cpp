@@ -566,7 +566,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
         {(void**)&ix->prep_err, 16},
         {(void**)&ix->dev.slice_rec, n * 32}, {(void**)&ix->dev.chunk_rec, n * 32},
-        {(void**)&ix->dev.item_tot, 16},     {(void**)&ix->dev.build_arrive, 16},
+        {(void**)&ix->dev.item_tot, 64},     {(void**)&ix->dev.build_arrive, 2048},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
         {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
         {(void**)&ix->dev.hseg, (size_t)(T0 * hs) * 8},

@@ -67,8 +67,8 @@ __device__ __forceinline__ f32x4 load_sc1(const float* p) {
 
 // The grad row of position p, vector k of this lane (k = v + j*64).
 template <typename GT>
-__device__ __forceinline__ typename Vec<GT>::type grad_vec(const GT* gbase, int64_t grad_ld, int L, int p, int k) {
-    return ldg<typename Vec<GT>::type>((const typename Vec<GT>::type*)(gbase + (int64_t)(p / L) * grad_ld) + k);
+__device__ __forceinline__ typename Vec<GT>::type grad_vec(const GT* gbase, int64_t grad_ld, const FastDiv& L, int p, int k) {
+    return ldg<typename Vec<GT>::type>((const typename Vec<GT>::type*)(gbase + (int64_t)L(p) * grad_ld) + k);
 }
 
 template <typename GT>
@@ -83,7 +83,7 @@ __device__ __forceinline__ void add_vec(float* acc, const typename Vec<GT>::type
 template <typename TT, typename GT, int VPR>
 __device__ __forceinline__ void run_chunk(const int32_t* __restrict__ perm, const int4& a, const int4& b,
                                           TT* __restrict__ table, const GT* __restrict__ gbase, int64_t grad_ld,
-                                          int L, float lr, int v, int gl0) {
+                                          const FastDiv& L, float lr, int v, int gl0) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE, D = G::D, LPR = G::LPR;
     constexpr int KX = (kChunk - kChunkInline + LPR - 1) / LPR;  // perm loads per lane (long chunks)
@@ -148,7 +148,7 @@ struct SinglesArgs {
 };
 template <typename TT, typename GT, int VPR>
 __device__ __forceinline__ void run_singles(const SinglesArgs& sa, int64_t cap, TT* __restrict__ table, int64_t nrows,
-                                            int t, int p0, const GT* __restrict__ gbase, int64_t grad_ld, int L,
+                                            int t, int p0, const GT* __restrict__ gbase, int64_t grad_ld, const FastDiv& L,
                                             float lr, int v, int gl0) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE, D = G::D, LPR = G::LPR, PPG = G::SPPG;
@@ -219,7 +219,7 @@ struct SliceLds {
 template <typename TT, typename GT, int VPR>
 __device__ __forceinline__ void slice_body(const int32_t* __restrict__ pos, int len, TT* __restrict__ row, int ns,
                                            float* part_me, const float* part_first, int64_t pdim, int32_t* cnt_p,
-                                           const GT* __restrict__ gbase, int64_t grad_ld, int L, float lr,
+                                           const GT* __restrict__ gbase, int64_t grad_ld, const FastDiv& L, float lr,
                                            SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
     typedef ApplyGeom<GT, VPR> G;
     constexpr int NE = G::NE, D = G::D, LPR = G::LPR, NG = G::NG;
@@ -316,7 +316,7 @@ __device__ __forceinline__ void slice_body(const int32_t* __restrict__ pos, int 
 // row, h}; the segment's descriptor ix.hot[vt][h] = {beg, end, row, first slice}
 template <typename TT, typename GT, int VPR>
 __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, const int4& sd, TT* __restrict__ table,
-                                          const GT* __restrict__ gbase, int64_t grad_ld, int L, float lr,
+                                          const GT* __restrict__ gbase, int64_t grad_ld, const FastDiv& L, float lr,
                                           SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
     constexpr int D = ApplyGeom<GT, VPR>::D;
     const int64_t off = (int64_t)vt * ix.cap;
@@ -328,15 +328,16 @@ __device__ __forceinline__ void run_slice(const IndexerDev& ix, int vt, int sl, 
                             ix.hot_cnt + off + sd.w, gbase, grad_ld, L, lr, sm);
 }
 
-// ---- flat hot slice k of the item map (one 32-B record: IndexerDev::slice_rec)
+// ---- hot slice k of the item map (one 32-B record: IndexerDev::slice_rec); k and its segment's
+// first slice `first` count over the sub-lists' slices in order (partial row and counter slots)
 template <typename TT, typename GT, int VPR>
-__device__ __forceinline__ void run_slice_rec(const IndexerDev& ix, int k, const int4& r0, const int4& r1,
+__device__ __forceinline__ void run_slice_rec(const IndexerDev& ix, int k, int first, const int4& r0, const int4& r1,
                                               TT* __restrict__ table, const GT* __restrict__ gbase, int64_t grad_ld,
-                                              int L, float lr, SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
+                                              const FastDiv& L, float lr, SliceLds<ApplyGeom<GT, VPR>::D>& sm) {
     constexpr int D = ApplyGeom<GT, VPR>::D;
     slice_body<TT, GT, VPR>(ix.perm + r0.x, r0.y - r0.x, table + (int64_t)(uint32_t)r0.z * D, r1.x,
-                            ix.partial + (int64_t)k * ix.pdim, ix.partial + (int64_t)r1.y * ix.pdim, ix.pdim,
-                            ix.hot_cnt + r1.y, gbase, grad_ld, L, lr, sm);
+                            ix.partial + (int64_t)k * ix.pdim, ix.partial + (int64_t)first * ix.pdim, ix.pdim,
+                            ix.hot_cnt + first, gbase, grad_ld, L, lr, sm);
 }
 
 }  // namespace dlrm

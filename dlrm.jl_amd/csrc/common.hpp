@@ -61,6 +61,22 @@ template <typename V> __device__ __forceinline__ void stg(void* p, const V& v) {
 template <typename V> __device__ __forceinline__ void stg_nt(void* p, const V& v) { *(V*)p = v; }
 #endif
 
+// n / d for 0 <= n < 2^31 and d >= 1 by a multiply-high, an add and a shift (the round-up magic:
+// m = floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d); exact over that range), set up once per
+// kernel: the apply's position -> bag (sample) for every grad row it reads, where the compiler's
+// division by a run-time L costs ~15 VALU per row.
+struct FastDiv {
+    uint32_t m;
+    int l;
+    __device__ __forceinline__ explicit FastDiv(int d) {
+        l = d > 1 ? 32 - __clz(d - 1) : 0;
+        m = (uint32_t)((((unsigned long long)1 << 32) * (((unsigned long long)1 << l) - (unsigned)d)) / (unsigned)d + 1);
+    }
+    __device__ __forceinline__ int operator()(int n) const {
+        return (int)((__umulhi(m, (uint32_t)n) + (uint32_t)n) >> l);
+    }
+};
+
 // Index i of an int32 / int64 index array, without a branch on the type: a branch per load
 // makes the compiler wait for each load at the join, serialising a lane's index loads.
 // (int32: the second word read is the first one again.)
@@ -243,17 +259,18 @@ struct IndexerDev {
     // indexed by v, and the apply maps v -> t.
     int vshift;
     int hbits;
-    // flat item lists of the wave build (apply.hpp reads them when has_map): every build wave
-    // reserves its hot slices and chunks and arrives with ONE 64-bit atomic add on build_arrive
-    // (indexer.hpp kRes*Shift packing) and writes them whole; the last wave to arrive copies the
-    // totals to item_tot = {hot slices, chunks} and clears the word.
+    // flat item lists of the wave build (apply.hpp reads them when has_map), in 8 sub-lists (by
+    // build workgroup mod 8): every build wave reserves its hot slices and chunks and arrives with
+    // ONE 64-bit atomic add on its sub-list's word of build_arrive (indexer.hpp kRes*) and writes
+    // them whole; a sub-list's last wave to arrive copies its totals to item_tot[j] (slices) /
+    // item_tot[8 + j] (chunks) and clears the word.
     //   slice_rec[2k, 2k+1]: {first perm entry, end (global: v * cap + local), row, v},
     //                        {slices of its segment, flat index of the segment's first slice, 0, 0}
     //   chunk_rec[2c, 2c+1]: the chunk descriptor (write_chunk) with global perm entries
     int4* slice_rec;
     int4* chunk_rec;
     int32_t* item_tot;
-    uint32_t* build_arrive;  // the reservation word (64 bits, 8-B aligned)
+    uint32_t* build_arrive;  // the reservation words (64 bits, 256 B apart)
     int has_map;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)

@@ -537,7 +537,7 @@ __device__ __forceinline__ void locate_in_tile(int incl, int tile_total, int tb,
 // of the G = ceil(T / 64) consecutive tables [l*G, l*G + G) and the inclusive prefix of their
 // sums, so a lookup is one binary lifting over the lanes plus G independent shuffles.  More
 // tables are re-scanned tile by tile on every lookup.
-constexpr int kScanTiles = 8;  // (T <= 512 virtual tables: the wave build's 16 parts of up to 32 tables)
+constexpr int kScanTiles = 2;  // (T <= 128 virtual tables; the wave build's 16-part tables use the item map)
 struct TableScan {
     int cnt[kScanTiles];  // counts of this lane's tables
     int incl;             // inclusive prefix over the lanes' groups
@@ -626,9 +626,27 @@ struct WaveBuildLds {
     int tot[kWaveParts][kWaveParts];  // [wave][part]: positions of the workgroup's part q that wave w read
 };
 
-// The flat item lists' reservation word (build_arrive, 64 bits): chunks in bits 0..23, hot slices
-// in 24..43, arrived build waves in 44..63 (the wave build: <= 31 x 2048 positions).
+// The flat item lists come in kResLists sub-lists: build workgroup g reserves in sub-list g mod 8
+// (its XCD's), so each reservation word takes an eighth of the build's atomics (one word took ~2.7
+// us to return with all 416 waves on it).  Word j (build_arrive, 64 bits, one per 256 B): chunks in
+// bits 0..23, hot slices in 24..43, arrived waves in 44..63 (the wave build: <= 31 x 2048
+// positions).  Sub-list j's records start at j * res_stride (a workgroup's positions, <= cap, give
+// at most cap / 2 chunks and as many slices); item_tot[j] / [kResLists + j] = its slices / chunks.
 constexpr int kResSliceShift = 24, kResArriveShift = 44;
+constexpr int kResLists = 8, kResWordStride = 32;  // (u64 words: 256 B apart)
+__device__ __forceinline__ int res_stride(int groups, int64_t cap) {
+    return ((groups + kResLists - 1) / kResLists) * (int)(cap / 2 + 8);
+}
+// flat record index of item k of the sub-lists with counts cnt[0..kResLists), or -1 past the end
+__device__ __forceinline__ int res_locate(const int* cnt, int k, int stride) {
+    int run = 0, at = -1;
+#pragma unroll
+    for (int j = 0; j < kResLists; ++j) {
+        if (at < 0 && k < run + cnt[j]) at = j * stride + (k - run);
+        run += cnt[j];
+    }
+    return at;
+}
 
 __device__ __forceinline__ unsigned long long lanes_below() {
     const int lane = threadIdx.x & 63;
@@ -697,8 +715,39 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
     return m;
 }
 
+// The first pass of a wide-key part, unstable: one LDS atomic per key on its low-byte counter
+// (a bucket's keys land in any order; wave_rank_buckets orders them by (key, position)).  Same
+// contract as wave_count_pass otherwise.
+__device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
+                                        int32_t* Vout, int32_t* R, uint32_t* cnt) {
+    const int lane = threadIdx.x & 63;
+    *(uint4*)&cnt[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) R[i] = (int)atomicAdd(&cnt[Kin[i] & 255u], 1u);
+    wave_lds_sync();
+    const uint4 c = *(const uint4*)&cnt[4 * lane];
+    const int sum = (int)(c.x + c.y + c.z + c.w);
+    int o = wave_incl_scan(sum) - sum;
+    uint4 st;
+    st.x = o; o += c.x;
+    st.y = o; o += c.y;
+    st.z = o; o += c.z;
+    st.w = o;
+    *(uint4*)&cnt[4 * lane] = st;
+    const int m = lane63(wave_incl_max((int)max(max(c.x, c.y), max(c.z, c.w))));
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) {
+        const uint32_t k = Kin[i];
+        const int dst = (int)cnt[k & 255u] + R[i];
+        Kout[dst] = k;
+        Vout[dst] = Vin[i];
+    }
+    wave_lds_sync();
+    return m;
+}
+
 // Every low-byte bucket small (uniform rows): each key's place in its bucket by a direct rank on
-// (key, position); the stable pass left each bucket in position order, so j < i <=> pos_j < pos_i.
+// (key, position) (positions are distinct, so the order is total and the sort stable).
 __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, uint32_t* K0, int32_t* V0,
                                   const uint32_t* start) {
     for (int i = threadIdx.x & 63; i < n; i += 64) {
@@ -706,9 +755,10 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
         const int d = ki & 255u;
         const int bs = (int)start[d], be = d < 255 ? (int)start[d + 1] : n;
         int rank = 0;
+        const int32_t vi = V1[i];
         for (int j = bs; j < be; ++j) {
             const uint32_t kj = K1[j];
-            rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+            rank += (kj < ki || (kj == ki && V1[j] < vi)) ? 1 : 0;
         }
         K0[bs + rank] = ki;
         V0[bs + rank] = V1[i];
@@ -716,15 +766,101 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
     wave_lds_sync();
 }
 
+// One lane's segment of a tile of the sorted part, as its flat record: kind 1 = a chunk (a =
+// {first perm entry, end (global), row, pos0}, b = {pos1 .. pos4}; idx = the wave's chunk
+// number), 2 = a hot segment (a = {beg, end (local), row}; idx = the wave's first slice, ns slices).
+struct SegRec {
+    int4 a, b;
+    int kind, idx, ns;
+};
+
+struct SegPass {
+    const IndexerDev& ix;
+    int v, vs;
+    uint32_t part;
+    int n, U;
+    const uint32_t* Ks;
+    const int32_t* Vs;
+    const int32_t* R;
+    int64_t off;
+
+    // segments [s0, s0 + 64): the per-part lists (seg_start, seg_row, chunks, hot, hot_slice) when
+    // `lists`, and this lane's flat record; c / h / sl0 run over the tiles
+    __device__ __forceinline__ SegRec tile(int s0, int& c, int& h, int& sl0, bool lists) const {
+        const int lane = threadIdx.x & 63;
+        const unsigned long long lt = lanes_below();
+        const int s = s0 + lane;
+        const bool ok = s < U;
+        const int beg = ok ? R[s] : 0;
+        const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
+        const int len = end - beg;
+        const bool isc = ok && len >= 2 && len <= kChunk;
+        const bool ish = ok && len > kChunk;
+        const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
+        const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
+        const int sincl = wave_incl_scan(ns);
+        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
+        SegRec r{};
+        r.kind = isc ? 1 : (ish ? 2 : 0);
+        r.ns = ns;
+        if (isc) {
+            int q[kChunkInline];
+#pragma unroll
+            for (int k = 0; k < kChunkInline; ++k) q[k] = beg + k < end ? Vs[beg + k] : -1;
+            r.idx = c + __popcll(cb & lt);
+            r.a = make_int4((int)off + beg, (int)off + end, row, q[0]);
+            r.b = make_int4(q[1], q[2], q[3], q[4]);
+        } else if (ish) {
+            r.idx = sl0 + sincl - ns;
+            r.a = make_int4(beg, end, row, 0);
+        }
+        if (lists) {
+            if (ok) {
+                ix.seg_start[(int64_t)v * (ix.cap + 1) + s] = beg;
+                ix.seg_row[off + s] = (uint32_t)row;
+            }
+            if (isc) {
+                int4* chunks = ix.chunks + 2 * off;
+                chunks[2 * r.idx] = make_int4(beg, end, row, r.a.w);
+                chunks[2 * r.idx + 1] = r.b;
+            }
+            if (ish) {
+                const int hi = h + __popcll(hb & lt);
+                ix.hot[off + hi] = make_int4(beg, end, row, r.idx);
+                for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice)
+                    ix.hot_slice[off + r.idx + k] = make_int4(p0, min(p0 + kHotSlice, end), row, hi);
+            }
+        }
+        c += __popcll(cb);
+        h += __popcll(hb);
+        sl0 += lane63(sincl);
+        return r;
+    }
+
+    __device__ __forceinline__ void flat(const SegRec& r, int cbase, int sbase) const {
+        if (r.kind == 1) {
+            ix.chunk_rec[2 * (int64_t)(cbase + r.idx)] = r.a;
+            ix.chunk_rec[2 * (int64_t)(cbase + r.idx) + 1] = r.b;
+        } else if (r.kind == 2) {
+            const int first = sbase + r.idx;
+            for (int k = 0, p0 = r.a.x; p0 < r.a.y; ++k, p0 += kHotSlice) {
+                ix.slice_rec[2 * (int64_t)(first + k)] =
+                    make_int4((int)off + p0, (int)off + min(p0 + kHotSlice, r.a.y), r.a.z, v);
+                ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(r.ns, first, 0, 0);
+            }
+        }
+    }
+};
+
 // The part the calling wave sorts and writes out: virtual table v = (t << vs) + part, its n keys
 // (row >> vs) and positions in position order at K0 / V0 (K1, V1, R: the same span of the pool's
-// other arrays, scratch).  Sorts them in LDS (one counting pass on the low 8 key bits, then a
-// within-bucket rank or, for skewed rows, the remaining LSD passes), classifies the segments
-// (LDS only), reserves the wave's ranges of the flat item lists and arrives in one packed atomic
+// other arrays, scratch).  Sorts them in LDS: keys wider than 8 bits by one unstable counting pass
+// on the low byte and a within-bucket rank on (key, position); narrow keys, or buckets too big to
+// rank (skewed rows), by stable LSD counting passes.  Then classifies the segments (LDS only), reserves the wave's ranges of the flat item lists and arrives in one packed atomic
 // add, stores the per-table outputs while it is in flight, then the flat records at its return.
 __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
                                int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, WaveBuildLds& sl,
-                               int groups) {
+                               int g, int groups) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lanes_below();
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
@@ -733,49 +869,53 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
-    if (n > 1 && nbits > 0) {
-        const int mb = wave_count_pass(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
+    if (n > 1 && nbits > 8 && wave_count_pass_unstable(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
+        WPH(3);
+        wave_rank_buckets(n, K1, V1, K0, V0, cnt);
+    } else if (n > 1 && nbits > 0) {  // narrow keys, or skewed rows: stable LSD passes from (K0, V0)
+        wave_count_pass(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
         WPH(3);
         Ks = K1;
         Vs = V1;
-        if (nbits > 8) {
-            if (mb <= kWaveRankMax) {
-                wave_rank_buckets(n, K1, V1, K0, V0, cnt);
-                Ks = K0;
-                Vs = V0;
-            } else {  // skewed rows: the remaining LSD passes
-                for (int shift = 8; shift < nbits; shift += 8) {
-                    const bool from1 = Ks == K1;
-                    wave_count_pass(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
-                                    from1 ? K0 : K1, from1 ? V0 : V1, R, cnt);
-                    Ks = from1 ? K0 : K1;
-                    Vs = from1 ? V0 : V1;
-                }
-            }
+        for (int shift = 8; shift < nbits; shift += 8) {
+            const bool from1 = Ks == K1;
+            wave_count_pass(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
+                            from1 ? K0 : K1, from1 ? V0 : V1, R, cnt);
+            Ks = from1 ? K0 : K1;
+            Vs = from1 ? V0 : V1;
         }
     }
     WPH(4);
-    // segment starts (R[s]) and counts, LDS only
-    int U = 0;
+    // One pass over the sorted keys: segment starts R[s] and the counts that size the wave's share
+    // of the flat lists -- chunks (a head that is not a tail and whose key differs kChunk places on:
+    // 2 .. kChunk positions) and hot segments (longer), whose slices are counted from R after.
+    int U = 0, C = 0, H = 0;
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int i = j0 + lane;
-        const bool head = i < n && (i == 0 || Ks[i - 1] != Ks[i]);
+        const bool ok = i < n;
+        const uint32_t k = ok ? Ks[i] : 0u;
+        const bool head = ok && (i == 0 || Ks[i - 1] != k);
+        const bool tail = ok && (i + 1 == n || Ks[i + 1] != k);
+        const bool longer = ok && i + kChunk < n && Ks[i + kChunk] == k;
         const unsigned long long hb = __ballot(head);
         if (head) R[U + __popcll(hb & lt)] = i;
+        C += __popcll(__ballot(head && !tail && !longer));
+        H += __popcll(__ballot(head && longer));
         U += __popcll(hb);
     }
     wave_lds_sync();
-    int C = 0, S = 0;
-    for (int s0 = 0; s0 < U; s0 += 64) {
-        const int s = s0 + lane;
-        const int len = s < U ? (s + 1 < U ? R[s + 1] : n) - R[s] : 0;
-        C += __popcll(__ballot(len >= 2 && len <= kChunk));
-        S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
-    }
+    int S = 0;
+    if (H)  // (rows hit more than kChunk times in this part: small tables)
+        for (int s0 = 0; s0 < U; s0 += 64) {
+            const int s = s0 + lane;
+            const int len = s < U ? (s + 1 < U ? R[s + 1] : n) - R[s] : 0;
+            S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
+        }
     // The wave reserves its flat-list ranges and arrives in ONE atomic add (lane 0), issued before
     // any store: the stores below run while it is in flight, and only the flat records wait for it.
     unsigned long long res = 0ull;
-    unsigned long long* word = (unsigned long long*)ix.build_arrive;
+    const int list = g & (kResLists - 1);
+    unsigned long long* word = (unsigned long long*)ix.build_arrive + list * kResWordStride;
     if (lane == 0) {
         // (a zero the compiler cannot see through: a uniform address gets the wave-aggregating
         // atomic rewrite, whose readfirstlane would wait for the return right here)
@@ -790,8 +930,6 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     // the outputs: perm, once-hit flags, segments, per-table chunk / hot lists, counts
     const int64_t off = (int64_t)v * ix.cap;
     int32_t* perm = ix.perm + off;
-    int32_t* seg_start = ix.seg_start + (int64_t)v * (ix.cap + 1);
-    uint32_t* seg_row = ix.seg_row + off;
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int i = j0 + lane;
@@ -804,82 +942,41 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
             single[p] = (head && tail) ? 1 : 0;
         }
     }
-    int4* chunks = ix.chunks + 2 * off;
-    int4* hot = ix.hot + off;
-    int4* hot_slice = ix.hot_slice + off;
+    WPH(9);
+    // segments: the first two tiles keep their flat records in registers for after the reservation
+    // returns; later tiles (U > 128) are recomputed then
+    SegPass sp{ix, v, vs, part, n, U, Ks, Vs, R, off};
     int c = 0, h = 0, sl0 = 0;
-    for (int s0 = 0; s0 < U; s0 += 64) {
-        const int s = s0 + lane;
-        const bool ok = s < U;
-        const int beg = ok ? R[s] : 0;
-        const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
-        const int len = end - beg;
-        const bool isc = ok && len >= 2 && len <= kChunk;
-        const bool ish = ok && len > kChunk;
-        const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
-        const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
-        const int sincl = wave_incl_scan(ns);
-        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
-        if (ok) {
-            seg_start[s] = beg;
-            seg_row[s] = (uint32_t)row;
-        }
-        if (isc) write_chunk(chunks, c + __popcll(cb & lt), beg, end, row, Vs);
-        if (ish) {
-            const int hi = h + __popcll(hb & lt), sloc = sl0 + sincl - ns;
-            hot[hi] = make_int4(beg, end, row, sloc);
-            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice)
-                hot_slice[sloc + k] = make_int4(p0, min(p0 + kHotSlice, end), row, hi);
-        }
-        c += __popcll(cb);
-        h += __popcll(hb);
-        sl0 += lane63(sincl);
-    }
+    const SegRec r0 = sp.tile(0, c, h, sl0, true);
+    const SegRec r1 = U > 64 ? sp.tile(64, c, h, sl0, true) : SegRec{};
+    const int c2 = c, s2 = sl0;
+    for (int s0 = 128; s0 < U; s0 += 64) (void)sp.tile(s0, c, h, sl0, true);
     if (lane == 0) {
-        seg_start[U] = n;
+        ix.seg_start[(int64_t)v * (ix.cap + 1) + U] = n;
         int32_t* cn = ix.counts + (int64_t)v * 8;
         cn[CNT_U] = U; cn[CNT_C] = c; cn[CNT_H] = h; cn[CNT_S] = sl0; cn[CNT_NV] = n;
     }
-    // the reservation's return: the wave's bases; the last of the groups x kWaveParts waves to
-    // arrive publishes the lists' totals and clears the word for this indexer's next build (read
-    // in a later launch)
+    // the reservation's return: the wave's bases in its sub-list; the sub-list's last wave to arrive
+    // publishes its totals and clears the word for this indexer's next build (read in a later launch)
     res = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(res >> 32)) << 32) |
           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)res);
-    const int cbase = (int)(res & ((1u << kResSliceShift) - 1u));
-    const int sbase = (int)((res >> kResSliceShift) & ((1u << (kResArriveShift - kResSliceShift)) - 1u));
-    if (lane == 0 && (unsigned)(res >> kResArriveShift) == (unsigned)(groups * kWaveParts - 1)) {
-        ix.item_tot[0] = sbase + S;
-        ix.item_tot[1] = cbase + C;
+    WPH(8);
+    const int cloc = (int)(res & ((1u << kResSliceShift) - 1u));
+    const int sloc = (int)((res >> kResSliceShift) & ((1u << (kResArriveShift - kResSliceShift)) - 1u));
+    const int lwaves = ((groups - list + kResLists - 1) / kResLists) * kWaveParts;  // this sub-list's
+    if (lane == 0 && (unsigned)(res >> kResArriveShift) == (unsigned)(lwaves - 1)) {
+        ix.item_tot[list] = sloc + S;
+        ix.item_tot[kResLists + list] = cloc + C;
         *word = 0ull;
     }
+    const int lbase = list * res_stride(groups, ix.cap);
+    const int cbase = lbase + cloc, sbase = lbase + sloc;
     // the flat records (chunk_rec, slice_rec) at the reserved ranges
-    c = 0;
-    sl0 = 0;
-    for (int s0 = 0; s0 < U; s0 += 64) {
-        const int s = s0 + lane;
-        const bool ok = s < U;
-        const int beg = ok ? R[s] : 0;
-        const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
-        const int len = end - beg;
-        const bool isc = ok && len >= 2 && len <= kChunk;
-        const bool ish = ok && len > kChunk;
-        const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
-        const unsigned long long cb = __ballot(isc);
-        const int sincl = wave_incl_scan(ns);
-        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
-        if (isc)
-            write_chunk_rec(ix.chunk_rec, (int64_t)cbase + c + __popcll(cb & lt), (int)(off + beg), (int)(off + end),
-                            row, Vs + beg);
-        if (ish) {
-            const int first = sbase + sl0 + sincl - ns;
-            for (int k = 0, p0 = beg; p0 < end; ++k, p0 += kHotSlice) {
-                ix.slice_rec[2 * (int64_t)(first + k)] = make_int4((int)(off + p0), (int)(off + min(p0 + kHotSlice, end)), row, v);
-                ix.slice_rec[2 * (int64_t)(first + k) + 1] = make_int4(ns, first, 0, 0);
-            }
-        }
-        c += __popcll(cb);
-        sl0 += lane63(sincl);
-    }
+    sp.flat(r0, cbase, sbase);
+    sp.flat(r1, cbase, sbase);
+    c = c2;
+    sl0 = s2;
+    for (int s0 = 128; s0 < U; s0 += 64) sp.flat(sp.tile(s0, c, h, sl0, false), cbase, sbase);
     WPH(6);
 }
 
@@ -1019,7 +1116,7 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     const int pb = pbase[w], n = n_of[w];
     const int v = (t << vs) + q0 + w;
     wave_sort_part(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
-                   sl.cnt[w], sl, (T << vs) / kWaveParts);
+                   sl.cnt[w], sl, g, (T << vs) / kWaveParts);
 }
 
 }  // namespace dlrm

@@ -383,6 +383,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     // a bounds error raised since the last dlrm_check_bounds (the lookup or the indexer build of
     // this step): the reference's gather throws before update!, so no table row is written.  (The
     // error word is loaded with the item counts, one round trip for both.)
+    const FastDiv Ld(L);  // position -> bag
     const unsigned err0 = ldg<unsigned>(err);
     typedef ApplyGeom<GT, VPR> G;
     constexpr int D = G::D, NG = G::NG;
@@ -395,9 +396,23 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     const bool mp = ix.has_map != 0;
     TableScan sS{}, sC{};
     int Stot, Ctot;
+    // the item map's sub-list counts (indexer.hpp kResLists), kept in LDS: item_tot[0..8) slices,
+    // [8..16) chunks
+    __shared__ int lcnt[2 * kResLists];
+    const int* ls = lcnt;
+    const int* lc = lcnt + kResLists;
+    int lstride = 0;
     if (mp) {
-        Stot = ix.item_tot[0];
-        Ctot = ix.item_tot[1];
+        if (threadIdx.x < 2 * kResLists) lcnt[threadIdx.x] = ix.item_tot[threadIdx.x];
+        __syncthreads();
+        Stot = 0;
+        Ctot = 0;
+#pragma unroll
+        for (int j = 0; j < kResLists; ++j) {
+            Stot += ls[j];
+            Ctot += lc[j];
+        }
+        lstride = res_stride(T_ / kWaveParts, ix.cap);
     } else {
         sS = scan_counts(ix, T_, CNT_S);
         sC = scan_counts(ix, T_, CNT_C);
@@ -449,7 +464,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
             if (g >= G::RPW) continue;
             const TableDesc td = load_table(tabs, t);
             run_singles<TT, GT, VPR>(sa, ix.cap, (TT*)td.data, td.nrows, t, p0, grad + grad_offset + (int64_t)t * D,
-                                     grad_ld, L, lr, v, lane - v);
+                                     grad_ld, Ld, lr, v, lane - v);
             APPLY_END();
             continue;
         }
@@ -460,8 +475,9 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
             int t;
             if (mp) {  // the flat chunk record: perm entries global, the virtual table = beg / cap
                 if (g >= G::RPW || fc >= Ctot) continue;
-                ca = ix.chunk_rec[2 * (int64_t)fc];
-                cb = ix.chunk_rec[2 * (int64_t)fc + 1];
+                const int r = res_locate(lc, fc, lstride);
+                ca = ix.chunk_rec[2 * (int64_t)r];
+                cb = ix.chunk_rec[2 * (int64_t)r + 1];
                 pbase = ix.perm;
                 t = (int)(ca.x / ix.cap) >> ix.vshift;
             } else {
@@ -474,16 +490,17 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
                 pbase = ix.perm + (int64_t)tc * ix.cap;
                 t = tc >> ix.vshift;
             }
-            run_chunk<TT, GT, VPR>(pbase, ca, cb, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, L,
+            run_chunk<TT, GT, VPR>(pbase, ca, cb, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, Ld,
                                    lr, v, lane - v);
             APPLY_END();
             continue;
         }
         if (mp) {  // (uniform: the slice's whole record in one 32-B load)
-            const int4 r0 = ix.slice_rec[2 * (int64_t)item], r1 = ix.slice_rec[2 * (int64_t)item + 1];
+            const int r = res_locate(ls, item, lstride);
+            const int4 r0 = ix.slice_rec[2 * (int64_t)r], r1 = ix.slice_rec[2 * (int64_t)r + 1];
             const int t = r0.w >> ix.vshift;
-            run_slice_rec<TT, GT, VPR>(ix, item, r0, r1, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D,
-                                       grad_ld, L, lr, sm);
+            run_slice_rec<TT, GT, VPR>(ix, item, item - (r - r1.y), r0, r1, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D,
+                                       grad_ld, Ld, lr, sm);
             APPLY_END();
             continue;
         }
@@ -491,7 +508,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
         locate(ix, T_, CNT_S, sS, item, th, sl);  // item < S: found, the same for every lane
         const int4 sd = ix.hot_slice[(int64_t)th * ix.cap + sl];
         const int t = th >> ix.vshift;
-        run_slice<TT, GT, VPR>(ix, th, sl, sd, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, L, lr,
+        run_slice<TT, GT, VPR>(ix, th, sl, sd, (TT*)tabs[t].data, grad + grad_offset + (int64_t)t * D, grad_ld, Ld, lr,
                                sm);
         APPLY_END();
     }

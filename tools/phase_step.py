@@ -104,3 +104,11 @@ if hasattr(lib, "dlrm_debug_wph"):
             if (col > 0).any():
                 r = rel[:, k][col > 0]
                 print(f"  mark {k:2d}: {np.percentile(r, 50):6.2f} / {r.max():6.2f}")
+        # the slowest waves: (group, wave, table rows, per-mark us)
+        gw = np.argwhere(np.array(wb, dtype=np.int64).reshape(256, 4, 16)[:int((kind == 4).sum()), :, 0] > 0)
+        ends = [(rel[i, 6] if a3[ok][i, 6] > 0 else 0.0, i) for i in range(rel.shape[0])]
+        for e, i in sorted(ends)[-8:]:
+            g_, w_ = gw[i]
+            t_ = int(g_) // 4
+            print(f"  slow wave g={int(g_)} w={int(w_)} table {t_} ({rows[t_]} rows):",
+                  {k: round(float(rel[i, k]), 2) for k in range(1, 16) if a3[ok][i, k] > 0})
