@@ -39,7 +39,8 @@ struct ApplyGeom {
     static constexpr int VPL = VPR <= 64 ? 1 : VPR / 64;
     static constexpr int RPW = 64 / LPR;
     static constexpr int NG = kApplyWaves * RPW;        // lane groups per workgroup
-    static constexpr int IF = VPL >= 4 ? 4 : 16 / VPL;  // grad rows in flight per lane
+    static constexpr int SIF = NE == 8 ? kSliceIF / 2 : kSliceIF;  // hot slice rows in flight (bf16: 8 per 16 B)
+    static constexpr int IF = VPL >= 4 ? 4 : (NE == 8 ? 8 : 16) / VPL;  // grad rows in flight per lane
     // once-hit positions per lane group (a grad and a table row in flight for each)
     static constexpr int SPPG = VPL * NE >= 16 ? 2 : (VPL * NE >= 8 ? 4 : 8);
 };
@@ -207,7 +208,6 @@ struct PrepArgs {
 // LDS of a hot-slice item (one workgroup)
 template <int D>
 struct SliceLds {
-    int32_t pos[kHotSlice];           // the slice's positions (perm[p0, p1))
     f32x4 wsum[kApplyWaves][D / 4];   // per-wave partial rows
     int last;
 };
@@ -229,26 +229,34 @@ __device__ __forceinline__ void slice_body(const int32_t* __restrict__ pos, int 
     // the table row, loaded now (needed only at the end; no other item writes it in this launch)
     float rw[4];
     if (tid < D / 4) load_row<TT, 4>(row, tid * 4, rw);
-    for (int i = tid; i < len; i += kApplyThreads) sm.pos[i] = pos[i];
-    __syncthreads();
-    // this group's consecutive share, in position order
+    // this group's consecutive share [g0, u1), in position order: lane v of the group loads
+    // positions g0 + k LPR + v, and each row's position comes by a shuffle (no LDS staging and no
+    // barrier before the grad rows)
+    const int g0 = gid * SPG, u1 = min(len, g0 + SPG);  // (SPG = kHotSlice / NG)
+    static_assert(SPG <= LPR, "one position per lane of the group");
+    const int gl0 = lane - v;
+    const int px = g0 + v < u1 ? pos[g0 + v] : 0;
     float acc[G::VPL][NE];
 #pragma unroll
     for (int j = 0; j < G::VPL; ++j)
 #pragma unroll
         for (int e = 0; e < NE; ++e) acc[j][e] = 0.0f;
-    const int u1 = min(len, (gid + 1) * SPG);  // (SPG = kHotSlice / NG)
     // grad rows in flight per lane: a lane group's whole share at one 16-B vector per row
     // up to kSliceIF, else the chunk items' IF
-    constexpr int IFS = G::VPL == 1 ? (SPG < kSliceIF ? SPG : kSliceIF) : G::IF;
+    constexpr int IFS = G::VPL == 1 ? (SPG < G::SIF ? SPG : G::SIF) : G::IF;
     constexpr int IF = IFS < SPG ? IFS : SPG;
-    for (int u0 = gid * SPG; u0 < u1; u0 += IF) {
+#pragma unroll 1
+    for (int r0 = 0; r0 < SPG; r0 += IF) {
+        const int u0 = g0 + r0;
+        if (u0 >= u1) break;  // uniform over the group
         typename Vec<GT>::type gv[IF][G::VPL];
 #pragma unroll
-        for (int uu = 0; uu < IF; ++uu)
+        for (int uu = 0; uu < IF; ++uu) {
+            const int p = __shfl(px, gl0 + r0 + uu, 64);
             if (u0 + uu < u1)
 #pragma unroll
-                for (int j = 0; j < G::VPL; ++j) gv[uu][j] = grad_vec<GT>(gbase, grad_ld, L, sm.pos[u0 + uu], v + j * 64);
+                for (int j = 0; j < G::VPL; ++j) gv[uu][j] = grad_vec<GT>(gbase, grad_ld, L, p, v + j * 64);
+        }
 #pragma unroll
         for (int uu = 0; uu < IF; ++uu)
             if (u0 + uu < u1)

@@ -617,12 +617,14 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
 // Output format = fast_index_table's (split): the apply, dlrm_indexer_read and the step backward
 // read it unchanged.  Within a part, segments come in ascending row order, positions ascending.
 constexpr int kWaveParts = 4;       // waves per build workgroup = parts of one table per workgroup
-constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-byte bucket is this small
+constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-digit bucket is this small
+constexpr int kWideDigit = 9;       // wide keys' first digit: 512 buckets for ~150 keys of a part
 struct WaveBuildLds {
-    uint32_t K[2][kStepIndexMaxN];  // keys (row >> vshift), sort ping-pong; the 4 parts' regions
-    int32_t V[2][kStepIndexMaxN];   // positions
-    int32_t R[kStepIndexMaxN];      // per-key rank in its digit, then segment starts
-    uint32_t cnt[kWaveParts][256];  // per-wave digit counters, then digit offsets
+    // (each part's region starts 16-B aligned: up to 3 entries of padding after each of 4 parts)
+    uint32_t K[2][kStepIndexMaxN + 16];  // keys (row >> vshift), sort ping-pong; the 4 parts' regions
+    int32_t V[2][kStepIndexMaxN + 16];   // positions
+    int32_t R[kStepIndexMaxN + 16];      // per-key rank in its digit, then segment starts
+    uint32_t cnt[kWaveParts][1 << kWideDigit];  // per-wave digit counters, then digit offsets
     int tot[kWaveParts][kWaveParts];  // [wave][part]: positions of the workgroup's part q that wave w read
 };
 
@@ -715,30 +717,48 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
     return m;
 }
 
-// The first pass of a wide-key part, unstable: one LDS atomic per key on its low-byte counter
-// (a bucket's keys land in any order; wave_rank_buckets orders them by (key, position)).  Same
-// contract as wave_count_pass otherwise.
+// The first pass of a wide-key part, unstable: one LDS atomic per key on the counter of its low
+// kWideDigit bits (a bucket's keys land in any order; wave_rank_buckets orders them by (key,
+// position)).  Leaves cnt[d] = the start of digit d's bucket; returns the largest bucket.
 __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
                                         int32_t* Vout, int32_t* R, uint32_t* cnt) {
+    constexpr uint32_t dm = (1u << kWideDigit) - 1u;
+    constexpr int PL = (1 << kWideDigit) / 64;  // counters per lane
+    static_assert(PL % 4 == 0, "whole uint4 per lane");
     const int lane = threadIdx.x & 63;
-    *(uint4*)&cnt[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* c4 = (uint4*)&cnt[PL * lane];
+#pragma unroll
+    for (int q = 0; q < PL / 4; ++q) c4[q] = make_uint4(0u, 0u, 0u, 0u);
     wave_lds_sync();
-    for (int i = lane; i < n; i += 64) R[i] = (int)atomicAdd(&cnt[Kin[i] & 255u], 1u);
+    for (int i = lane; i < n; i += 64) R[i] = (int)atomicAdd(&cnt[Kin[i] & dm], 1u);
     wave_lds_sync();
-    const uint4 c = *(const uint4*)&cnt[4 * lane];
-    const int sum = (int)(c.x + c.y + c.z + c.w);
+    uint32_t c[PL];
+#pragma unroll
+    for (int q = 0; q < PL / 4; ++q) {
+        const uint4 x = c4[q];
+        c[4 * q] = x.x; c[4 * q + 1] = x.y; c[4 * q + 2] = x.z; c[4 * q + 3] = x.w;
+    }
+    int sum = 0, mx = 0;
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+        sum += (int)c[q];
+        mx = max(mx, (int)c[q]);
+    }
     int o = wave_incl_scan(sum) - sum;
-    uint4 st;
-    st.x = o; o += c.x;
-    st.y = o; o += c.y;
-    st.z = o; o += c.z;
-    st.w = o;
-    *(uint4*)&cnt[4 * lane] = st;
-    const int m = lane63(wave_incl_max((int)max(max(c.x, c.y), max(c.z, c.w))));
+#pragma unroll
+    for (int q = 0; q < PL / 4; ++q) {
+        uint4 st;
+        st.x = o; o += c[4 * q];
+        st.y = o; o += c[4 * q + 1];
+        st.z = o; o += c[4 * q + 2];
+        st.w = o; o += c[4 * q + 3];
+        c4[q] = st;
+    }
+    const int m = lane63(wave_incl_max(mx));
     wave_lds_sync();
     for (int i = lane; i < n; i += 64) {
         const uint32_t k = Kin[i];
-        const int dst = (int)cnt[k & 255u] + R[i];
+        const int dst = (int)cnt[k & dm] + R[i];
         Kout[dst] = k;
         Vout[dst] = Vin[i];
     }
@@ -746,14 +766,15 @@ __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_
     return m;
 }
 
-// Every low-byte bucket small (uniform rows): each key's place in its bucket by a direct rank on
+// Every low-digit bucket small (uniform rows): each key's place in its bucket by a direct rank on
 // (key, position) (positions are distinct, so the order is total and the sort stable).
 __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, uint32_t* K0, int32_t* V0,
                                   const uint32_t* start) {
+    constexpr int dm = (1 << kWideDigit) - 1;
     for (int i = threadIdx.x & 63; i < n; i += 64) {
         const uint32_t ki = K1[i];
-        const int d = ki & 255u;
-        const int bs = (int)start[d], be = d < 255 ? (int)start[d + 1] : n;
+        const int d = (int)(ki & (uint32_t)dm);
+        const int bs = (int)start[d], be = d < dm ? (int)start[d + 1] : n;
         int rank = 0;
         const int32_t vi = V1[i];
         for (int j = bs; j < be; ++j) {
@@ -886,22 +907,57 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
         }
     }
     WPH(4);
-    // One pass over the sorted keys: segment starts R[s] and the counts that size the wave's share
-    // of the flat lists -- chunks (a head that is not a tail and whose key differs kChunk places on:
-    // 2 .. kChunk positions) and hot segments (longer), whose slices are counted from R after.
+    // One pass over the sorted keys, four consecutive keys per lane (16-B LDS reads: the part's
+    // region starts 16-B aligned): perm and the once-hit flags stored, segment starts R[s], and the
+    // counts that size the wave's share of the flat lists -- chunks (a head that is not a tail and
+    // whose key differs kChunk places on: 2 .. kChunk positions) and hot segments (longer), whose
+    // slices are counted from R after.  (Its stores precede the reservation atomic below; they
+    // complete before it returns anyway.)
+    const int64_t off = (int64_t)v * ix.cap;
+    int32_t* perm = ix.perm + off;
+    uint8_t* single = ix.single + (int64_t)t * ix.cap;
+    const bool pvec = (ix.cap & 3) == 0;  // perm + i 16-B aligned
     int U = 0, C = 0, H = 0;
-    for (int j0 = 0; j0 < n; j0 += 64) {
-        const int i = j0 + lane;
-        const bool ok = i < n;
-        const uint32_t k = ok ? Ks[i] : 0u;
-        const bool head = ok && (i == 0 || Ks[i - 1] != k);
-        const bool tail = ok && (i + 1 == n || Ks[i + 1] != k);
-        const bool longer = ok && i + kChunk < n && Ks[i + kChunk] == k;
-        const unsigned long long hb = __ballot(head);
-        if (head) R[U + __popcll(hb & lt)] = i;
-        C += __popcll(__ballot(head && !tail && !longer));
-        H += __popcll(__ballot(head && longer));
-        U += __popcll(hb);
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        const int i = j0 + 4 * lane;
+        const uint4 k4 = *(const uint4*)(Ks + i);  // (past n: garbage, masked below)
+        const int4 v4 = *(const int4*)(Vs + i);
+        const uint4 kf = *(const uint4*)(Ks + i + kChunk);
+        const uint32_t kp = Ks[i > 0 ? i - 1 : 0], kn = Ks[i + 4];
+        const uint32_t kk[6] = {kp, k4.x, k4.y, k4.z, k4.w, kn};
+        const uint32_t kfa[4] = {kf.x, kf.y, kf.z, kf.w};
+        const int vv[4] = {v4.x, v4.y, v4.z, v4.w};
+        int nh = 0, nc = 0, nhot = 0;
+        bool hd[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int ie = i + e;
+            const bool ok = ie < n;
+            const bool head = ok && (ie == 0 || kk[e] != kk[e + 1]);
+            const bool tail = ok && (ie + 1 == n || kk[e + 2] != kk[e + 1]);
+            const bool longer = ok && ie + kChunk < n && kfa[e] == kk[e + 1];
+            hd[e] = head;
+            nh += head ? 1 : 0;
+            nc += (head && !tail && !longer) ? 1 : 0;
+            nhot += (head && longer) ? 1 : 0;
+            if (ok) single[vv[e]] = (head && tail) ? 1 : 0;
+        }
+        if (pvec && i + 3 < n)
+            *(int4*)(perm + i) = v4;
+        else
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (i + e < n) perm[i + e] = vv[e];
+        // (three 10-bit fields: <= 256 per tile)
+        const int packed = nh | (nc << 10) | (nhot << 20);
+        const int incl = wave_incl_scan(packed), tot = lane63(incl);
+        int at = U + ((incl - packed) & 1023);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (hd[e]) R[at++] = i + e;
+        U += tot & 1023;
+        C += (tot >> 10) & 1023;
+        H += tot >> 20;
     }
     wave_lds_sync();
     int S = 0;
@@ -911,8 +967,8 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
             const int len = s < U ? (s + 1 < U ? R[s + 1] : n) - R[s] : 0;
             S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
         }
-    // The wave reserves its flat-list ranges and arrives in ONE atomic add (lane 0), issued before
-    // any store: the stores below run while it is in flight, and only the flat records wait for it.
+    // The wave reserves its flat-list ranges and arrives in ONE atomic add (lane 0): the segment
+    // stores below run while it is in flight, and only the flat records wait for it.
     unsigned long long res = 0ull;
     const int list = g & (kResLists - 1);
     unsigned long long* word = (unsigned long long*)ix.build_arrive + list * kResWordStride;
@@ -927,21 +983,6 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     WPH(5);
-    // the outputs: perm, once-hit flags, segments, per-table chunk / hot lists, counts
-    const int64_t off = (int64_t)v * ix.cap;
-    int32_t* perm = ix.perm + off;
-    uint8_t* single = ix.single + (int64_t)t * ix.cap;
-    for (int j0 = 0; j0 < n; j0 += 64) {
-        const int i = j0 + lane;
-        if (i < n) {
-            const uint32_t k = Ks[i];
-            const bool head = i == 0 || Ks[i - 1] != k;
-            const bool tail = i + 1 == n || Ks[i + 1] != k;
-            const int p = Vs[i];
-            perm[i] = p;
-            single[p] = (head && tail) ? 1 : 0;
-        }
-    }
     WPH(9);
     // segments: the first two tiles keep their flat records in registers for after the reservation
     // returns; later tiles (U > 128) are recomputed then
@@ -1084,7 +1125,7 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
             pbase[q] = run;
             woff[q] = wq;
             n_of[q] = nq;
-            run += nq;
+            run += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
         }
     }
     WPH(1);
