@@ -69,7 +69,12 @@ struct FastDiv {
     uint32_t m;
     int l;
     __device__ __forceinline__ explicit FastDiv(int d) {
-        l = d > 1 ? 32 - __clz(d - 1) : 0;
+        if (d <= 1) {  // (one-hot: no 64-bit division at the kernel's start)
+            m = 1u;
+            l = 0;
+            return;
+        }
+        l = 32 - __clz(d - 1);
         m = (uint32_t)((((unsigned long long)1 << 32) * (((unsigned long long)1 << l) - (unsigned)d)) / (unsigned)d + 1);
     }
     __device__ __forceinline__ int operator()(int n) const {
