@@ -617,7 +617,7 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
 // Output format = fast_index_table's (split): the apply, dlrm_indexer_read and the step backward
 // read it unchanged.  Within a part, segments come in ascending row order, positions ascending.
 constexpr int kWaveParts = 4;       // waves per build workgroup = parts of one table per workgroup
-constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-digit bucket is this small
+constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-digit bucket is this small (256: Terabyte Zipf rows 17.3 -> 33.4 us apply, each hot-bucket lane walks the whole bucket)
 constexpr int kWideDigit = 9;       // wide keys' first digit: 512 buckets for ~150 keys of a part
 struct WaveBuildLds {
     // (each part's region starts 16-B aligned: up to 3 entries of padding after each of 4 parts)
@@ -775,14 +775,23 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
         const uint32_t ki = K1[i];
         const int d = (int)(ki & (uint32_t)dm);
         const int bs = (int)start[d], be = d < dm ? (int)start[d + 1] : n;
-        int rank = 0;
         const int32_t vi = V1[i];
-        for (int j = bs; j < be; ++j) {
-            const uint32_t kj = K1[j];
-            rank += (kj < ki || (kj == ki && V1[j] < vi)) ? 1 : 0;
+        // four bucket entries per 16-B read pair (the part's region is 16-B aligned), so a skewed
+        // bucket (a hot row: ~100+ keys) costs a quarter of the read latencies
+        int rank = 0;
+        for (int j0 = bs & ~3; j0 < be; j0 += 4) {
+            const uint4 kq = *(const uint4*)(K1 + j0);
+            const int4 vq = *(const int4*)(V1 + j0);
+            const uint32_t kj[4] = {kq.x, kq.y, kq.z, kq.w};
+            const int32_t vj[4] = {vq.x, vq.y, vq.z, vq.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = j0 + e;
+                rank += (j >= bs && j < be && (kj[e] < ki || (kj[e] == ki && vj[e] < vi))) ? 1 : 0;
+            }
         }
         K0[bs + rank] = ki;
-        V0[bs + rank] = V1[i];
+        V0[bs + rank] = vi;
     }
     wave_lds_sync();
 }

@@ -18,12 +18,21 @@ lib = pkg._lib.load(os.environ["DLRM_HIP_LIB"])
 dev = torch.device("cuda:0")
 D = int(os.environ.get("D", "128"))
 B = int(os.environ.get("B", "2048"))
-rows = pkg.KAGGLE_EMBEDDING_SIZES
+# WL=tb: Terabyte-like Zipf(1.05) rows (row counts capped at 2^24 to keep the tables small; the key
+# widths stay > 8 bits, so the build takes the same paths)
+WL = os.environ.get("WL", "kaggle")
+rows = pkg.KAGGLE_EMBEDDING_SIZES if WL == "kaggle" else [min(n, 1 << 24) for n in pkg.TERABYTE_EMBEDDING_SIZES]
 tabs = [torch.zeros((n, D), device=dev) for n in rows]
 ts = pkg.EmbeddingTableSet(tabs)
 g = torch.Generator(device=dev).manual_seed(1)
-packs = [pkg.PackedIndices(torch.stack([torch.randint(0, n, (B,), device=dev, generator=g) for n in rows])
-                           .to(torch.int32)) for _ in range(4)]
+if WL == "kaggle":
+    packs = [pkg.PackedIndices(torch.stack([torch.randint(0, n, (B,), device=dev, generator=g) for n in rows])
+                               .to(torch.int32)) for _ in range(4)]
+else:
+    rng = np.random.default_rng(1)
+    perms = [pkg.zipf_perm(rng, n) for n in rows]
+    packs = [pkg.PackedIndices(torch.from_numpy(np.stack([pkg.zipf_rows(rng, n, B, 1.05, p) for n, p in zip(rows, perms)]))
+                               .to(dev)) for _ in range(4)]
 hp = pkg.HotPath(ts, B, 1, lr=0.01, index_base=0, pipeline="apply")
 x = torch.randn((B, D), device=dev)
 dout = torch.randn((B, hp.width), device=dev) * 1e-3
