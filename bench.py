@@ -464,6 +464,7 @@ def main():
         try:
             for k in range(2):
                 chain_step(k)
+            ht.flush()  # (update! is deferred into the next maplookup's launch; a graph piece ends flushed)
             gs = {}
             for piece in set(plan(a.steps)) | set(plan(a.warmup)):
                 cur = torch.cuda.current_stream()
@@ -474,6 +475,7 @@ def main():
                     with torch.cuda.graph(gr, stream=s_):
                         for k in range(piece[0], piece[0] + piece[1]):
                             chain_step(k)
+                        ht.flush()
                 cur.wait_stream(s_)
                 gs[piece] = gr
             for piece in plan(a.warmup):
@@ -488,7 +490,9 @@ def main():
             chain = {"value": round(B / (ms_c / 1e3), 1), "ms_per_step": round(ms_c, 4),
                      "vs_step": round(ms / ms_c, 3),
                      "form": "maplookup(HipTables) -> rrule(DotInteraction) -> pullback -> maplookup_pullback -> "
-                             "update!(Descent): dlrm_step_fwd / dlrm_step_bwd(BWD_ONLY) / (APPLY_ONLY), hipGraph replay"}
+                             "update!(Descent; check_bounds=false): dlrm_step_fwd / dlrm_step_bwd(BWD_ONLY) / the "
+                             "deferred update!'s apply launch, run by the next maplookup with that batch's indexer "
+                             "build (dlrm_step_bwd_prepare(APPLY_ONLY)), hipGraph replay"}
         except Exception as e:
             print(f"note: drop-in chain timing failed ({e!r})", file=sys.stderr)
 

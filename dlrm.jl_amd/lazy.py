@@ -22,6 +22,12 @@ DLRMHip.jl's lazy `maplookup` for `HipEmbedding`):
                           known η, dlrm_sgd_update(PREBUILT) with the forward's split indexer
 
 Three launches per step, bit for bit the result of `HotPath.step` and of the five-launch chain.
+
+With the learning rate known and `update!(…; check_bounds=false)` (the training loop's form), the
+apply launch is deferred to the next `maplookup` on these tables, which then runs it together
+with the build of its own batch's indexer (dlrm_step_bwd_prepare with STEP_APPLY_ONLY): the
+forward that follows only gathers -- the pipelined step's three launches.  Every read of the
+tables through `HipTables` (`ts`, indexing, iteration, `flush()`) runs a pending update first.
 Anything else that reads ys gets it materialized (`LazyLookup.materialize`).  `out`, `dx` and the
 gradient live in per-batch-size buffers reused by the next step, as the reference's own
 preallocated scratch (`DotInteraction`'s per-thread scratchpads) is.
@@ -36,11 +42,39 @@ class HipTables:
     interaction.  lr: the Descent η the following update! will use (lets the backward apply the
     once-hit rows itself, the fastest form); None: update! applies every row."""
 
-    def __init__(self, tables, *, lr=None, index_base=1):
-        self.ts = as_table_set(tables) if not isinstance(tables, EmbeddingTableSet) else tables
+    def __init__(self, tables, *, lr=None, index_base=1, defer_update=True):
+        self._ts = as_table_set(tables) if not isinstance(tables, EmbeddingTableSet) else tables
         self.lr = None if lr is None else float(lr)
         self.index_base = int(index_base)  # 1: Julia's, as maplookup / update_ default to
+        self.defer_update = bool(defer_update)
         self._hp = {}
+        self._spare = {}      # batch -> the second indexer of the pipelined form
+        self._pending = None  # the LazyGrad whose apply launch is deferred to the next maplookup
+
+    @property
+    def ts(self):
+        """The EmbeddingTableSet, with any deferred update applied."""
+        self.flush()
+        return self._ts
+
+    def flush(self, next_idx=None):
+        """Runs a deferred update!'s apply launch.  next_idx (the next maplookup's PackedIndices):
+        the same launch builds their split indexer, so the next forward only gathers."""
+        lz = self._pending
+        if lz is None:
+            return
+        self._pending = None
+        hp = lz.hp
+        if (next_idx is not None and next_idx.L == 1 and next_idx.B == lz.idx.B and
+                (next_idx.itype, next_idx.stride) == (lz.idx.itype, lz.idx.stride)):
+            nix = self._spare.get(hp.B)
+            if nix is None:
+                from .update import SparseIndexer
+                nix = self._spare[hp.B] = SparseIndexer(hp.T, hp.B, hp.ts.device)
+            hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY, prepare=(nix, next_idx))
+            self._spare[hp.B], hp.indexer = hp.indexer, nix  # the next forward reads the prepared one
+        else:
+            hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY)
 
     def check_index_base(self, index_base, op):
         """A caller-passed index base must be the tables' own (None: the tables')."""
@@ -49,7 +83,7 @@ class HipTables:
                              f"index_base={self.index_base}")
 
     def __len__(self):
-        return len(self.ts)
+        return len(self._ts)
 
     def __iter__(self):
         return iter(self.ts)
@@ -59,14 +93,14 @@ class HipTables:
 
     @property
     def D(self):
-        return self.ts.D
+        return self._ts.D
 
     def hotpath(self, batch):
         """The preallocated step state of one batch size (buffers, indexer)."""
         from .hotpath import HotPath
         hp = self._hp.get(batch)
         if hp is None:
-            hp = HotPath(self.ts, batch, 1, lr=0.0 if self.lr is None else self.lr, index_base=self.index_base)
+            hp = HotPath(self._ts, batch, 1, lr=0.0 if self.lr is None else self.lr, index_base=self.index_base)
             if not hp.step_api:
                 raise ValueError("HipTables: this table set has no training-step kernels (deterministic, one-hot)")
             self._hp[batch] = hp
@@ -86,11 +120,11 @@ class LazyLookup:
 
     @property
     def dtype(self):
-        return self.tables.ts.dtype
+        return self.tables._ts.dtype
 
     @property
     def device(self):
-        return self.tables.ts.device
+        return self.tables._ts.device
 
     def materialize(self, check_bounds=None):
         """The ys the reference's maplookup returns (one dlrm_maplookup launch)."""
@@ -140,10 +174,11 @@ class DeferredUpdate(SparseEmbeddingUpdate):
 def maplookup_lazy(strategy, tables, sparse, check_bounds=True):
     """(Bounds of a LazyLookup's indices are raised by the fused forward's flag: at update_ with
     check_bounds, or at the next check_bounds.)"""
-    idx = PackedIndices(sparse, device=tables.ts.device)
+    idx = PackedIndices(sparse, device=tables._ts.device)
     if idx.T != len(tables):
         raise ValueError(f"{idx.T} index arrays for {len(tables)} tables")
     if isinstance(strategy, PreallocationStrategy) and idx.L == 1:
+        tables.flush(next_idx=idx)  # a deferred update's apply, with this batch's indexer build
         return LazyLookup(tables, idx, strategy.prealloc, check_bounds)
     # pooled bags / DefaultStrategy: the plain operator (no fused step form)
     from .embedding import maplookup
@@ -182,9 +217,13 @@ def update_lazy(opt, tables, grads, *, check_bounds=True):
     if len(grads) != len(tables) or any(g.lazy is not lz or g.table_index != t for t, g in enumerate(grads)):
         raise ValueError("update_ expects the per-table views of one maplookup pullback")
     hp = lz.hp
+    tables.flush()
     if lz.applied:
         if opt.eta != tables.lr:
             raise ValueError(f"the pullback stepped the once-hit rows with η = {tables.lr}; update! got {opt.eta}")
+        if tables.defer_update and not check_bounds:
+            tables._pending = lz  # applied by the next maplookup's launch (or any read of the tables)
+            return tables
         hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY)
     else:
         hp.lr = opt.eta

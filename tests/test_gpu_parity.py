@@ -687,6 +687,47 @@ def test_drop_in_operator_chain_on_step_kernels(pkg, gpu, rows, D, B, lr_known):
         assert e.value.code == pkg._lib.E_STATE
 
 
+def test_drop_in_chain_deferred_update(pkg, gpu):
+    """update!(...; check_bounds=false) on HipTables with a known η defers its apply launch to the
+    next maplookup, which runs it together with the build of its own batch's indexer (the
+    pipelined step): over three steps out, dx and every table equal HotPath.step bit for bit, a
+    read of the tables runs the pending update first, and the second and third forwards found
+    their indexer prepared."""
+    rows, D, B = pkg.KAGGLE_EMBEDDING_SIZES, 128, 2048
+    rng = np.random.default_rng(41)
+    T = len(rows)
+    tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
+    idxs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+            for _ in range(3)]
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    lr = 0.25
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr, index_base=0)
+    dot = pkg.DotInteraction()
+    used = []
+    for p in idxs:
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p, index_base=0)
+        used.append(ht.hotpath(B).indexer)
+        out, back = pkg.rrule(dot, x, ys)
+        _, dx, dy = back(dout)
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), index_base=0, check_bounds=False)
+        assert ht._pending is not None  # deferred
+    got = [to_np_f32(t.data) for t in ht.ts]  # the read runs the last pending update
+    assert ht._pending is None
+    assert used[1] is not used[0] and used[2] is used[0]  # two indexers alternate (prepared forwards)
+    torch.cuda.synchronize()
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=0)
+    for p in idxs:
+        hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_f32(out), to_np_f32(hp.out))
+    assert np.array_equal(to_np_f32(dx), to_np_f32(hp.dx))
+    for a, b in zip(got, hp.ts):
+        assert np.array_equal(a, to_np_f32(b.data))
+    ht.hotpath(B).check_bounds()
+
+
 def test_step_api_state_and_bounds(pkg, gpu):
     """The forward's split indexer also drives the plain update (once-hit rows included, bit for
     bit the update of a fresh build); step_bwd needs step_fwd's indices; an out-of-range index
