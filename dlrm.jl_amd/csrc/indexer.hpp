@@ -719,7 +719,8 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
 
 // The first pass of a wide-key part, unstable: one LDS atomic per key on the counter of its low
 // kWideDigit bits (a bucket's keys land in any order; wave_rank_buckets orders them by (key,
-// position)).  Leaves cnt[d] = the start of digit d's bucket; returns the largest bucket.
+// position)).  Leaves cnt[d] = the start of digit d's bucket; returns the largest bucket (and places
+// nothing when it exceeds kWaveRankMax).
 __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
                                         int32_t* Vout, int32_t* R, uint32_t* cnt) {
     constexpr uint32_t dm = (1u << kWideDigit) - 1u;
@@ -756,6 +757,7 @@ __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_
     }
     const int m = lane63(wave_incl_max(mx));
     wave_lds_sync();
+    if (m > kWaveRankMax) return m;  // (skewed: the caller re-sorts (Kin, Vin) by stable passes)
     for (int i = lane; i < n; i += 64) {
         const uint32_t k = Kin[i];
         const int dst = (int)cnt[k & dm] + R[i];
