@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=640)
     ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--graph-steps", type=int, default=CHUNK,
+                    help="steps per captured hipGraph, rounded down to whole cycles over the index batches "
+                         "(the per-replay launch gap is paid once per graph)")
     ap.add_argument("--workload", default="kaggle-d128-b2048")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: the global batch (split evenly over the ranks; e.g. configs[3]: "
@@ -350,7 +353,9 @@ def main():
     # The timed K steps replay graphs of exactly the steps they stand for: full CHUNK-step graphs
     # plus one graph of the remainder (captured once here, outside the timed region).
     nb = a.nbatch
-    chunk = min(CHUNK, nb)
+    # (a whole number of cycles over the nb index batches, so every piece starts at batch 0, the
+    # state the pipelined indexer is primed to)
+    chunk = nb * max(1, a.graph_steps // nb)
     graphs = {}
     def prime():
         """Pipelined steps: the indexer the first step of a run reads holds batch 0 (a run starts
@@ -435,7 +440,9 @@ def main():
     # short K does not hide clock ramp or cache effects; reported beside value, not instead of it
     sustained = None
     if a.sustain > 0:
+        per = chunk // nb  # (whole graphs: every piece of the run was captured)
         cyc = max(1, int(np.ceil(a.sustain * 1e3 / (ms * nb))))
+        cyc = per * int(np.ceil(cyc / per))
         if world > 1:  # every rank runs the same number of steps
             tc = torch.tensor([cyc], device=dev)
             dist.all_reduce(tc, op=dist.ReduceOp.MAX)
