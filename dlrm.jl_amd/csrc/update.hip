@@ -356,6 +356,11 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 // balances, and no workgroup is launched past the work.
 // MODE 0: chunks + hot slices; 1: + once-hit (singles) items; 2: + the next batch's split indexer
 // in the first pa.T << pa.ix.vshift workgroups (PrepArgs).
+#ifndef DLRM_BUILD_PRIO
+#define DLRM_BUILD_PRIO 3
+#endif
+constexpr int kBuildPrio = DLRM_BUILD_PRIO;  // s_setprio of the in-apply build's waves (0..3)
+
 template <typename TT, typename GT, int VPR, int MODE>
 __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_,
                                                                   int L, const GT* __restrict__ grad, int64_t grad_ld,
@@ -368,6 +373,10 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
         extern __shared__ __attribute__((aligned(16))) unsigned char prep_lds[];
         const int NI = (pa.T << pa.ix.vshift) / kWaveParts;
         if (bid < NI) {  // the next batch's split build: one wave per table part (indexer.hpp)
+            // the build's waves first at the issue arbiter: its chain of dependent LDS / VALU steps is
+            // the launch's longest, the apply waves beside it mostly wait on memory (A/B on one box:
+            // 54.72 / 54.77 -> 54.91 / 55.04 M samples/s, apply 10.58 -> 10.45 us)
+            __builtin_amdgcn_s_setprio(kBuildPrio);
             ITEM_START(4, 0, bid);
             wave_build_group(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
                              *(WaveBuildLds*)prep_lds);
