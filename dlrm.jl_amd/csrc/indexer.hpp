@@ -617,7 +617,12 @@ __device__ __forceinline__ void locate(const IndexerDev& ix, int T_, int which, 
 // Output format = fast_index_table's (split): the apply, dlrm_indexer_read and the step backward
 // read it unchanged.  Within a part, segments come in ascending row order, positions ascending.
 constexpr int kWaveParts = 4;       // waves per build workgroup = parts of one table per workgroup
-constexpr int kWaveRankMax = 16;    // within-bucket rank when every low-digit bucket is this small (256: Terabyte Zipf rows 17.3 -> 33.4 us apply, each hot-bucket lane walks the whole bucket)
+#ifndef DLRM_WAVE_RANK_MAX
+#define DLRM_WAVE_RANK_MAX 16
+#endif
+// within-bucket rank when every low-digit bucket is this small (256: Terabyte Zipf rows 17.3 ->
+// 33.4 us apply, each hot-bucket lane walks the whole bucket)
+constexpr int kWaveRankMax = DLRM_WAVE_RANK_MAX;
 constexpr int kWideDigit = 9;       // wide keys' first digit: 512 buckets for ~150 keys of a part
 struct WaveBuildLds {
     // (each part's region starts 16-B aligned: up to 3 entries of padding after each of 4 parts)
