@@ -460,13 +460,16 @@ def main():
         ht = pkg.HipTables(ts, lr=a.lr, index_base=0)
         dot = pkg.DotInteraction()
         strat = pkg.PreallocationStrategy(D)
+        indexers = pkg.SparseIndexer(T, B, dev)  # train.jl:279 (accepted; the step carries its own)
 
         def chain_step(k):
             p = packs[k % nb]
             ys = pkg.maplookup(strat, ht, p)
             _, back = pkg.rrule(dot, x, ys)
             _, _, dy = back(dout)
-            pkg.update_(pkg.Descent(a.lr), ht, pkg.maplookup_pullback(D, ht, p, dy), check_bounds=False)
+            # the reference's call, train.jl:283-290 (no extra keyword): deferred by the tables' policy
+            pkg.update_(pkg.Descent(a.lr), ht, pkg.maplookup_pullback(D, ht, p, dy), indexers, num_splits=8,
+                        nthreads=12)
 
         try:
             for k in range(2):
@@ -493,13 +496,15 @@ def main():
                 gs[piece].replay()
             torch.cuda.synchronize()
             ms_c = (time.perf_counter() - t0) * 1e3 / a.steps
-            ht.hotpath(B).check_bounds()
+            ht.check_bounds()
             chain = {"value": round(B / (ms_c / 1e3), 1), "ms_per_step": round(ms_c, 4),
                      "vs_step": round(ms / ms_c, 3),
                      "form": "maplookup(HipTables) -> rrule(DotInteraction) -> pullback -> maplookup_pullback -> "
-                             "update!(Descent; check_bounds=false): dlrm_step_fwd / dlrm_step_bwd(BWD_ONLY) / the "
-                             "deferred update!'s apply launch, run by the next maplookup with that batch's indexer "
-                             "build (dlrm_step_bwd_prepare(APPLY_ONLY)), hipGraph replay"}
+                             "update!(Descent(η), tables, grads, indexers; num_splits, nthreads) as train.jl:283-290 "
+                             "calls it: dlrm_step_fwd / dlrm_step_bwd(BWD_ONLY, which also copies the bounds flag to "
+                             "host memory) / the deferred update!'s apply launch, run by the next maplookup with that "
+                             "batch's indexer build (dlrm_step_bwd_prepare(APPLY_ONLY)); no host sync per step; "
+                             "hipGraph replay"}
         except Exception as e:
             print(f"note: drop-in chain timing failed ({e!r})", file=sys.stderr)
 

@@ -53,6 +53,8 @@ SIGNATURES = {
     "dlrm_last_error": (ctypes.c_char_p, [_vp]),
     "dlrm_sync": (_i32, [_vp]),
     "dlrm_check_bounds": (_i32, [_vp]),
+    "dlrm_error_snapshot": (_i32, [_vp]),
+    "dlrm_error_peek": (_i32, [_vp, _vp]),
     "dlrm_malloc": (_i32, [_vp, _sz, _pp]),
     "dlrm_free": (_i32, [_vp, _vp]),
     "dlrm_memcpy_h2d": (_i32, [_vp, _vp, _vp, _sz]),

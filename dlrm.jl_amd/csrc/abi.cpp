@@ -25,6 +25,10 @@ struct dlrm_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     unsigned* err = nullptr;  // device error word
+    // host-visible copy of it (pinned), refreshed by dlrm_error_snapshot on the stream and read by
+    // dlrm_error_peek without touching the GPU: bounds errors of deferred work reach the host
+    // without a per-step synchronisation
+    volatile unsigned* err_host = nullptr;
     int cus = 256;
     char msg[512] = {0};
 };
@@ -151,8 +155,22 @@ int dlrm_ctx_create(int device, void* stream, dlrm_ctx** out) {
     }
     if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMalloc((void**)&ctx->err, 16), "hipMalloc(err)");
     if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemset(ctx->err, 0, 16), "hipMemset(err)");
+    if (rc == DLRM_OK) {
+        void* h = nullptr;
+        rc = ctx_hip(ctx, hipHostMalloc(&h, 64, hipHostMallocMapped), "hipHostMalloc(err_host)");
+        if (rc == DLRM_OK) {
+            memset(h, 0, 64);
+            ctx->err_host = (volatile unsigned*)h;
+            void* dh = nullptr;  // its device address, kept in the error word's second half
+            rc = ctx_hip(ctx, hipHostGetDevicePointer(&dh, h, 0), "hipHostGetDevicePointer(err_host)");
+            if (rc == DLRM_OK)
+                rc = ctx_hip(ctx, hipMemcpy((char*)ctx->err + 8, &dh, sizeof(dh), hipMemcpyHostToDevice),
+                             "write err_host address");
+        }
+    }
     if (rc != DLRM_OK) {
         if (ctx->err) (void)hipFree(ctx->err);
+        if (ctx->err_host) (void)hipHostFree((void*)ctx->err_host);
         delete ctx;
         return rc;
     }
@@ -166,6 +184,7 @@ int dlrm_ctx_destroy(dlrm_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->err_host) (void)hipHostFree((void*)ctx->err_host);
     delete ctx;
     return DLRM_OK;
 }
@@ -192,7 +211,21 @@ int dlrm_check_bounds(dlrm_ctx* ctx) {
     if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemsetAsync(ctx->err, 0, sizeof(unsigned), ctx->stream), "clear error word");
     if (rc == DLRM_OK) rc = ctx_hip(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     if (rc != DLRM_OK) return rc;
+    ctx->err_host[0] = 0;  // (the flag is clear now; a stale snapshot must not report it again)
     if (h & kErrIndex) return ctx_fail(ctx, DLRM_E_INDEX, "BoundsError: an embedding index was out of range");
+    return DLRM_OK;
+}
+
+int dlrm_error_snapshot(dlrm_ctx* ctx) {
+    if (!ctx) return DLRM_E_ARG;
+    return ctx_hip(ctx, hipMemcpyAsync((void*)ctx->err_host, ctx->err, sizeof(unsigned), hipMemcpyDeviceToHost,
+                                       ctx->stream),
+                   "dlrm_error_snapshot");
+}
+
+int dlrm_error_peek(const dlrm_ctx* ctx, unsigned* word) {
+    if (!ctx || !word) return DLRM_E_ARG;
+    *word = ctx->err_host[0];
     return DLRM_OK;
 }
 

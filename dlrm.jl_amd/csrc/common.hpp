@@ -21,6 +21,14 @@ constexpr int kArgTables = 32;
 // Device-side error word: bit 0 = an out-of-range index was skipped.
 constexpr unsigned kErrIndex = 1u;
 
+// The ctx's error word is 16 bytes: [0] the flag, [2..3] the device address of a host-memory copy
+// of it (dlrm_ctx_create).  One thread of a step backward (the launch after the forward that raises
+// the flag) stores the flag there, so the host reads it without a GPU call (dlrm_error_peek).
+__device__ __forceinline__ void snapshot_error(const unsigned* err, unsigned v) {
+    unsigned* h = *reinterpret_cast<unsigned* const*>(err + 2);
+    if (h) __hip_atomic_store(h, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void raise_index_error(unsigned* err) {
     __hip_atomic_fetch_or(err, kErrIndex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

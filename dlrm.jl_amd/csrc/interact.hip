@@ -391,6 +391,7 @@ __device__ __forceinline__ void bwd_body(int bid, int nblocks, float* smem, int 
             // a bounds error of this step (raised by the forward): the reference's gather throws
             // before update!, so every row goes to dt and the apply (which checks too) writes none
             const bool frozen = *su.err != 0;
+            if (b == 0 && lane == 0) snapshot_error(su.err, frozen ? 1u : 0u);
             uint8_t fl[NB][4];
             int64_t ui[NB][4];
 #pragma unroll
@@ -690,6 +691,7 @@ __global__ __launch_bounds__(64 * WPS * SPB, CPL == 8 ? 3 : (NB > 2 ? 2 : 4)) vo
             xv[sbi][k] = to_f32(ldg<T>(ob + (n < d ? n : 0)));
         }
     const bool frozen = su.single ? *su.err != 0 : true;  // a bounds error this step: no table row is written
+    if (su.single && blockIdx.x == 0 && threadIdx.x == 0) snapshot_error(su.err, frozen ? 1u : 0u);
     if (tdl_ok) {
         tds[threadIdx.x] = tdl;
         if constexpr (MAPPED) {

@@ -23,11 +23,17 @@ DLRMHip.jl's lazy `maplookup` for `HipEmbedding`):
 
 Three launches per step, bit for bit the result of `HotPath.step` and of the five-launch chain.
 
-With the learning rate known and `update!(…; check_bounds=false)` (the training loop's form), the
-apply launch is deferred to the next `maplookup` on these tables, which then runs it together
-with the build of its own batch's indexer (dlrm_step_bwd_prepare with STEP_APPLY_ONLY): the
-forward that follows only gathers -- the pipelined step's three launches.  Every read of the
-tables through `HipTables` (`ts`, indexing, iteration, `flush()`) runs a pending update first.
+With the learning rate known, `update!` is deferred by default (`HipTables(..., defer_update=True)`, a
+property of the tables, so the reference's own call `update!(opt, tables, grads, indexers; num_splits,
+nthreads)` defers unchanged): its apply launch runs in the next `maplookup` on these tables, together
+with the build of that batch's indexer (dlrm_step_bwd_prepare with STEP_APPLY_ONLY), so the forward
+that follows only gathers -- the pipelined step's three launches, with no host synchronisation.
+Bounds errors keep the reference's outcome (BoundsError, and no row of the failing step written):
+the kernels skip every table write once the device flag is set, the step backward copies the flag
+into host memory (one thread's store), and the next `maplookup` reads that copy without touching
+the GPU (dlrm_error_peek) and raises BoundsError when it is set -- one step or more after
+the failing one, the tables still in the state before it.  `check_bounds()` and every read of the
+tables through `HipTables` (`ts`, indexing, iteration) run a pending update and synchronise.
 Anything else that reads ys gets it materialized (`LazyLookup.materialize`).  `out`, `dx` and the
 gradient live in per-batch-size buffers reused by the next step, as the reference's own
 preallocated scratch (`DotInteraction`'s per-thread scratchpads) is.
@@ -40,7 +46,11 @@ from .update import Descent, SparseEmbeddingUpdate
 class HipTables:
     """Vector{HipEmbedding{Static{D}}}: embedding tables whose lookup is deferred into the
     interaction.  lr: the Descent η the following update! will use (lets the backward apply the
-    once-hit rows itself, the fastest form); None: update! applies every row."""
+    once-hit rows itself, the fastest form); None: update! applies every row.  defer_update: with
+    lr known, update! leaves its apply launch to the next maplookup (bounds errors surface there,
+    from a snapshot of the device flag, or at check_bounds / a read of the tables); False: update!
+    runs it at once and synchronises to check bounds, as the reference's update! returns with the
+    tables written."""
 
     def __init__(self, tables, *, lr=None, index_base=1, defer_update=True):
         self._ts = as_table_set(tables) if not isinstance(tables, EmbeddingTableSet) else tables
@@ -50,12 +60,29 @@ class HipTables:
         self._hp = {}
         self._spare = {}      # batch -> the second indexer of the pipelined form
         self._pending = None  # the LazyGrad whose apply launch is deferred to the next maplookup
+        self._unchecked = False  # deferred steps whose bounds flag has not been checked yet
 
     @property
     def ts(self):
-        """The EmbeddingTableSet, with any deferred update applied."""
-        self.flush()
+        """The EmbeddingTableSet, with any deferred update applied and its bounds checked (a read of
+        the tables is a host-visible point: BoundsError here if a deferred step had a bad index)."""
+        self.check_bounds()
         return self._ts
+
+    def check_bounds(self):
+        """Runs a deferred update, synchronises and raises BoundsError if any step since the last
+        check skipped an out-of-range index (its rows, and those of every later step, unwritten)."""
+        self.flush()
+        self._unchecked = False
+        self._ts.ctx.check_bounds()
+
+    def poll_bounds(self):
+        """No GPU call: raises BoundsError if the last error-flag snapshot that has landed is set.
+        A pending update of a failed step is dropped (the kernels skipped its writes anyway)."""
+        if self._unchecked and self._ts.ctx.error_peek():
+            self._pending = None
+            self._unchecked = False
+            self._ts.ctx.check_bounds()  # synchronises, clears the flag, raises
 
     def flush(self, next_idx=None):
         """Runs a deferred update!'s apply launch.  next_idx (the next maplookup's PackedIndices):
@@ -63,7 +90,6 @@ class HipTables:
         lz = self._pending
         if lz is None:
             return
-        self._pending = None
         hp = lz.hp
         if (next_idx is not None and next_idx.L == 1 and next_idx.B == lz.idx.B and
                 (next_idx.itype, next_idx.stride) == (lz.idx.itype, lz.idx.stride)):
@@ -75,6 +101,7 @@ class HipTables:
             self._spare[hp.B], hp.indexer = hp.indexer, nix  # the next forward reads the prepared one
         else:
             hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY)
+        self._pending = None  # (only once the apply launch was queued: a failed call keeps it pending)
 
     def check_index_base(self, index_base, op):
         """A caller-passed index base must be the tables' own (None: the tables')."""
@@ -137,6 +164,9 @@ class LazyLookup:
     def interact(self, x):
         if x.shape[1] != self.prealloc:
             raise ValueError(f"the interaction's x has {x.shape[1]} columns, maplookup reserved {self.prealloc}")
+        # an update! deferred after this lookup was made (out of the train! order) runs first: the
+        # forward must read the updated tables, and it rebuilds the indexer that update reads
+        self.tables.flush()
         hp = self.tables.hotpath(self.idx.B)
         hp.validate(x, self.idx)
         hp.step_fwd(x, self.idx)
@@ -178,6 +208,7 @@ def maplookup_lazy(strategy, tables, sparse, check_bounds=True):
     if idx.T != len(tables):
         raise ValueError(f"{idx.T} index arrays for {len(tables)} tables")
     if isinstance(strategy, PreallocationStrategy) and idx.L == 1:
+        tables.poll_bounds()  # a deferred step's BoundsError, from the flag snapshot (no GPU call)
         tables.flush(next_idx=idx)  # a deferred update's apply, with this batch's indexer build
         return LazyLookup(tables, idx, strategy.prealloc, check_bounds)
     # pooled bags / DefaultStrategy: the plain operator (no fused step form)
@@ -209,8 +240,10 @@ def pullback_lazy(strategy_prealloc, tables, dy):
     return [DeferredUpdate(dy, t, strategy_prealloc) for t in range(len(tables))]
 
 
-def update_lazy(opt, tables, grads, *, check_bounds=True):
-    """update!(Descent(η), ::HipTables, grads): the apply launch of the step."""
+def update_lazy(opt, tables, grads, *, check_bounds=None):
+    """update!(Descent(η), ::HipTables, grads): the apply launch of the step.  check_bounds: None
+    (the reference's call): the tables' policy -- deferred apply + flag snapshot when they defer,
+    else the launch and a synchronising check; True: run it now and check; False: no check."""
     if not isinstance(opt, Descent):
         raise TypeError("update_ implements Descent (plain SGD), the optimizer DLRM.jl trains with")
     lz = grads[0].lazy
@@ -223,11 +256,15 @@ def update_lazy(opt, tables, grads, *, check_bounds=True):
             raise ValueError(f"the pullback stepped the once-hit rows with η = {tables.lr}; update! got {opt.eta}")
         if tables.defer_update and not check_bounds:
             tables._pending = lz  # applied by the next maplookup's launch (or any read of the tables)
+            # (the step backward that ran in the pullback already copied the bounds flag as of this
+            # step's forward into host memory, for poll_bounds: no launch, no synchronisation here)
+            tables._unchecked = tables._unchecked or check_bounds is None
             return tables
         hp.step_bwd(lz.delta, x=lz.x, idx=lz.idx, flags=_lib.STEP_APPLY_ONLY)
     else:
         hp.lr = opt.eta
         hp.sgd_update(lz.idx, prebuilt=True)  # the forward's split indexer: once-hit rows as singles items
-    if check_bounds:
+    if check_bounds or check_bounds is None:
+        tables._unchecked = False
         hp.check_bounds()
     return tables

@@ -37,6 +37,16 @@ class Context:
         """Synchronises and raises BoundsError if a kernel skipped an out-of-range index."""
         self.check(self.lib.dlrm_check_bounds(self.bind()))
 
+    def error_snapshot(self):
+        """Queues a copy of the device error flag into host memory (no synchronisation; capturable)."""
+        self.check(self.lib.dlrm_error_snapshot(self.bind()))
+
+    def error_peek(self):
+        """The last snapshot of the error flag that has landed (no GPU call; 0 = none seen)."""
+        w = ctypes.c_uint()
+        self.check(self.lib.dlrm_error_peek(self.handle, ctypes.byref(w)))
+        return w.value
+
     def __del__(self):
         try:
             if self.handle:

@@ -150,14 +150,16 @@ class SparseIndexer:
 
 
 def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, index_base=None, deterministic=True,
-            prebuilt=False, check_bounds=True):
+            prebuilt=False, check_bounds=None):
     """EmbeddingTables.update!(opt, tables, grads, indexers; num_splits, nthreads).
 
     `grads` are the SparseEmbeddingUpdates of maplookup_pullback (they share one gradient
     matrix and one PackedIndices, so all tables update in one launch).  num_splits/nthreads
     are accepted for signature parity; the GPU decomposition is chunk-based.
     index_base: 1 (Julia) unless given; HipTables carry their own (a different one raises).
-    Tables are mutated in place."""
+    Tables are mutated in place.  check_bounds (not a reference keyword): None = the default --
+    synchronise and raise BoundsError for plain tables; HipTables follow their own policy (a
+    deferred apply whose bounds surface at the next maplookup, lazy.py)."""
     del num_splits, nthreads
     from .lazy import DeferredUpdate, HipTables, update_lazy
     if isinstance(tables, HipTables) and grads and isinstance(grads[0], DeferredUpdate):
@@ -203,6 +205,6 @@ def update_(opt, tables, grads, indexers=None, *, num_splits=8, nthreads=12, ind
     ctx.check(ctx.lib.dlrm_sgd_update(ctx.bind(), ts.handle, ix.handle if ix is not None else None, flags,
                                       ptr(idx.data), idx.itype, idx.stride, index_base, idx.B, idx.L, ptr(grad),
                                       dtype_code(grad.dtype), grad.stride(0), g0.grad_offset, opt.eta))
-    if check_bounds:
+    if check_bounds or check_bounds is None:
         ctx.check_bounds()
     return tables

@@ -86,6 +86,16 @@ int dlrm_sync(dlrm_ctx* ctx);
 /* Synchronises, reads and clears the device out-of-range flag raised by any kernel since
  * the previous call.  DLRM_E_INDEX if it was set. */
 int dlrm_check_bounds(dlrm_ctx* ctx);
+/* Bounds errors without a per-step synchronisation (the deferred update! of the drop-in chain).
+ * The step backward (dlrm_step_bwd / _prepare, backward launch) copies the flag into host memory
+ * owned by the ctx as it reads it (one thread's store); for other sequences
+ * dlrm_error_snapshot queues a copy of the device flag into host memory owned by the ctx (on the
+ * ctx stream; capturable, no synchronisation); dlrm_error_peek reads the last copy that has landed
+ * (no GPU call; 0 = no error seen yet).  A kernel that finds the device flag set writes no table
+ * row, so the tables keep the state before the failing step until dlrm_check_bounds reports and
+ * clears the flag (it also clears the host copy). */
+int dlrm_error_snapshot(dlrm_ctx* ctx);
+int dlrm_error_peek(const dlrm_ctx* ctx, unsigned* word);
 
 /* ---- device memory (so a host language without ROCm bindings can own buffers) ------- */
 int dlrm_malloc(dlrm_ctx* ctx, size_t bytes, void** dptr);

@@ -688,11 +688,11 @@ def test_drop_in_operator_chain_on_step_kernels(pkg, gpu, rows, D, B, lr_known):
 
 
 def test_drop_in_chain_deferred_update(pkg, gpu):
-    """update!(...; check_bounds=false) on HipTables with a known η defers its apply launch to the
-    next maplookup, which runs it together with the build of its own batch's indexer (the
-    pipelined step): over three steps out, dx and every table equal HotPath.step bit for bit, a
-    read of the tables runs the pending update first, and the second and third forwards found
-    their indexer prepared."""
+    """update!(opt, tables, grads, indexers) -- the reference's own call, no extra keyword -- on
+    HipTables with a known η defers its apply launch to the next maplookup, which runs it together
+    with the build of its own batch's indexer (the pipelined step): over three steps out, dx and
+    every table equal HotPath.step bit for bit, a read of the tables runs the pending update first,
+    and the second and third forwards found their indexer prepared."""
     rows, D, B = pkg.KAGGLE_EMBEDDING_SIZES, 128, 2048
     rng = np.random.default_rng(41)
     T = len(rows)
@@ -707,11 +707,12 @@ def test_drop_in_chain_deferred_update(pkg, gpu):
     dot = pkg.DotInteraction()
     used = []
     for p in idxs:
-        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p, index_base=0)
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p)
         used.append(ht.hotpath(B).indexer)
         out, back = pkg.rrule(dot, x, ys)
         _, dx, dy = back(dout)
-        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), index_base=0, check_bounds=False)
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), pkg.SparseIndexer(T, B, gpu),
+                    num_splits=8, nthreads=12)
         assert ht._pending is not None  # deferred
     got = [to_np_f32(t.data) for t in ht.ts]  # the read runs the last pending update
     assert ht._pending is None
@@ -726,6 +727,95 @@ def test_drop_in_chain_deferred_update(pkg, gpu):
     for a, b in zip(got, hp.ts):
         assert np.array_equal(a, to_np_f32(b.data))
     ht.hotpath(B).check_bounds()
+
+
+@pytest.mark.parametrize("sync_before_next", [True, False])
+def test_drop_in_chain_deferred_bounds_error(pkg, gpu, sync_before_next):
+    """The deferred update! keeps the reference's bounds outcome without a per-step host sync: a
+    batch with one out-of-range index raises BoundsError at a later maplookup (from the flag
+    snapshot, no GPU call) or at check_bounds, and no row of that step -- nor of any step queued
+    after it -- is written: the tables equal one good step.  After the error the chain trains on."""
+    rows, D, B = [3, 40, 100000, 7, 2_000_000], 64, 512
+    rng = np.random.default_rng(43)
+    T = len(rows)
+    tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
+    good = rand_indices(rng, rows, B, 1)
+    bad = rand_indices(rng, rows, B, 1)
+    bad[2, B // 2] = rows[2] + 5
+    p_good = pkg.PackedIndices(torch.from_numpy(good).to(torch.int32).to(gpu))
+    p_bad = pkg.PackedIndices(torch.from_numpy(bad).to(torch.int32).to(gpu))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    lr = 0.5
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr, index_base=0)
+    dot = pkg.DotInteraction()
+
+    def chain(p):
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p)
+        _, back = pkg.rrule(dot, x, ys)
+        _, _, dy = back(dout)
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy))
+
+    chain(p_good)
+    chain(p_bad)
+    assert ht._pending is not None
+    if sync_before_next:  # the snapshot has landed: the next maplookup raises without a GPU call
+        torch.cuda.synchronize()
+    raised = False
+    try:  # (without the sync the host may run ahead: the step queues and writes nothing)
+        chain(p_good)
+    except pkg.BoundsError:
+        raised = True
+    assert raised or not sync_before_next
+    if not raised:
+        with pytest.raises(pkg.BoundsError):
+            ht.check_bounds()
+    assert ht._pending is None
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=0)
+    hp.step(x, p_good, dout)
+    torch.cuda.synchronize()
+    for a, b in zip(ht.ts, hp.ts):  # (ts: flushed and checked -- clean now)
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data)), "a row of a BoundsError step was written"
+    chain(p_good)  # the flag is clear: the chain trains again
+    hp.step(x, p_good, dout)
+    torch.cuda.synchronize()
+    for a, b in zip(ht.ts, hp.ts):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
+
+
+def test_lazy_lookup_interacted_after_a_deferred_update(pkg, gpu):
+    """a LazyLookup made before a deferred update! and interacted after it reads the
+    updated tables (the pending apply runs first) and the update is not lost: two steps in this
+    order equal two HotPath steps."""
+    rows, D, B = [3, 40, 100000, 7], 32, 256
+    rng = np.random.default_rng(44)
+    T = len(rows)
+    tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
+    p0, p1 = (pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+              for _ in range(2))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=0.5, index_base=0)
+    dot = pkg.DotInteraction()
+    ys0 = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p0)
+    _, back = pkg.rrule(dot, x, ys0)
+    _, _, dy = back(dout)
+    ys1_early = pkg.LazyLookup(ht, p1, D)  # made while nothing is pending ...
+    pkg.update_(pkg.Descent(0.5), ht, pkg.maplookup_pullback(D, ht, p0, dy))
+    assert ht._pending is not None  # ... and interacted after the deferred update!
+    out1, back = pkg.rrule(dot, x, ys1_early)
+    _, dx1, dy = back(dout)
+    pkg.update_(pkg.Descent(0.5), ht, pkg.maplookup_pullback(D, ht, p1, dy))
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.5, index_base=0)
+    hp.step(x, p0, dout)
+    hp.step(x, p1, dout)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_np_f32(out1), to_np_f32(hp.out))
+    assert np.array_equal(to_np_f32(dx1), to_np_f32(hp.dx))
+    for a, b in zip(ht.ts, hp.ts):
+        assert np.array_equal(to_np_f32(a.data), to_np_f32(b.data))
 
 
 def test_step_api_state_and_bounds(pkg, gpu):

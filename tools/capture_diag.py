@@ -1,0 +1,180 @@
+"""Where does a captured RCCL exchange stop?  (capture_full hangs on a one-rank
+communicator.)  Runs one variant per child process with a stack-dumping timeout, printing a marker
+before and after every host call, so the log shows whether the host blocks inside the call
+(ncclGroupEnd / all_to_all_single), inside capture_end (graph instantiate), or on the device
+(replay + synchronize never returns).  The parent stops at the first variant that does not finish.
+
+    python tools/capture_diag.py OUTDIR variant[,variant...]
+
+variants: abi-eager, abi-op[:mode], torch-op[:mode], abi-step[:mode], torch-step[:mode]
+(mode = torch.cuda.graph capture_error_mode: global (default) | thread_local | relaxed)
+"""
+import faulthandler
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def mark(s):
+    print(f"[{time.perf_counter():.3f}] {s}", flush=True)
+
+
+def child(variant):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import dlrm_pkg
+    pkg = dlrm_pkg.load()
+    name, _, mode = variant.partition(":")
+    mode = mode or "global"
+    faulthandler.dump_traceback_later(40, exit=False)
+    gpu = torch.device("cuda:0")
+    torch.cuda.set_device(gpu)
+    kind, what = name.split("-")
+    if kind == "torch":
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=gpu)
+        mark("torch pg up")
+    T, B, D = 5, 128, 32
+    if what in ("eager", "op"):
+        send = torch.randn((T * B * D,), device=gpu)
+        recv = torch.empty_like(send)
+        if kind == "abi":
+            from dlrm_jl_amd.comm import CommExchange
+            comm = CommExchange(0, 1, gpu)
+            mark("comm up")
+
+            def op():
+                comm.alltoall_fwd(send, recv, D, B, [T])
+        else:
+            def op():
+                dist.all_to_all_single(recv, send, [T * B * D], [T * B * D])
+        op()
+        torch.cuda.synchronize()
+        mark(f"eager exchange ok: {torch.equal(recv, send)}")
+        if what == "eager":
+            return
+        recv.zero_()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            mark(f"capture_begin (mode {mode})")
+            g.capture_begin(capture_error_mode=mode)
+            mark("in capture: calling the exchange")
+            op()
+            mark("in capture: exchange call returned")
+            g.capture_end()
+            mark("capture_end returned (graph instantiated)")
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        mark("synced after capture")
+        g.replay()
+        mark("replay launched")
+        torch.cuda.synchronize()
+        mark(f"replay synced: equal={torch.equal(recv, send)}")
+        return
+    # the whole sharded step (tests/test_gpu_parity.py::test_sharded_whole_step_graph_world1)
+    from helpers import rand_indices, rand_tables
+    from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
+    rows, D, B, L = [3, 5000, 70, 100000, 11], 32, 128, 1
+    T = len(rows)
+    rng = np.random.default_rng(23)
+    tabs = rand_tables(rng, rows, D)
+    idx = pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, L)).to(torch.int32).reshape(T, B, L).to(gpu))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
+    eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind)
+    eng.step(x, idx, dout)
+    torch.cuda.synchronize()
+    mark("eager step ok")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        mark(f"capture_begin (mode {mode})")
+        g.capture_begin(capture_error_mode=mode)
+        eng._side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(eng._side):
+            eng.seg_index(idx)
+            eng._ix_done.record(eng._side)
+        mark("in capture: side-stream index build recorded")
+        eng.seg_lookup(idx, 0)
+        mark("in capture: lookup recorded")
+        eng.exchange_fwd(0)
+        mark("in capture: forward exchange returned")
+        eng.seg_interact(x, dout, 0)
+        mark("in capture: interaction recorded")
+        eng.exchange_bwd(0)
+        mark("in capture: backward exchange returned")
+        torch.cuda.current_stream().wait_event(eng._ix_done)
+        eng.seg_update(idx)
+        mark("in capture: update recorded")
+        g.capture_end()
+        mark("capture_end returned")
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g.replay()
+    mark("replay launched")
+    torch.cuda.synchronize()
+    mark("replay synced")
+
+
+def proc_state(pid):
+    out = []
+    try:
+        for tid in sorted(os.listdir(f"/proc/{pid}/task"), key=int):
+            def rd(f):
+                try:
+                    with open(f"/proc/{pid}/task/{tid}/{f}") as fh:
+                        return fh.read().strip()
+                except Exception as e:
+                    return f"?{e.__class__.__name__}"
+            comm = rd("comm")
+            out.append(f"  tid {tid} {comm:16s} wchan={rd('wchan')} syscall={rd('syscall').split(' ')[0]}")
+    except Exception as e:
+        out.append(f"  ({e!r})")
+    return "\n".join(out)
+
+
+def main():
+    outdir, variants = sys.argv[1], sys.argv[2].split(",")
+    os.makedirs(outdir, exist_ok=True)
+    for v in variants:
+        log = os.path.join(outdir, f"diag_{v.replace(':', '_')}.log")
+        env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "INFO"))
+        with open(log, "w") as fh:
+            p = subprocess.Popen([sys.executable, "-u", __file__, "--child", v], stdout=fh, stderr=subprocess.STDOUT,
+                                 env=env)
+            t0 = time.time()
+            while p.poll() is None and time.time() - t0 < 60:
+                time.sleep(0.5)
+            if p.poll() is None:
+                st = proc_state(p.pid)
+                p.kill()
+                p.wait()
+                fh.write("\n== TIMEOUT at 60 s; thread states before the kill:\n" + st + "\n")
+                print(f"{v}: TIMEOUT (log {log})", flush=True)
+                print(st, flush=True)
+                sys.exit(3)
+            print(f"{v}: rc={p.returncode} ({time.time() - t0:.1f} s)", flush=True)
+            if p.returncode != 0:
+                sys.exit(4)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+    else:
+        main()
