@@ -47,11 +47,13 @@ def parse():
                          "weak scaling, the workload's batch per GPU")
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
-                         "0: the engine's default (1: DESIGN.md §6)")
-    ap.add_argument("--shard-graph", choices=["full", "segments"], default="segments",
-                    help="multi-GPU graph form: 'full' = one hipGraph per step with the RCCL all-to-alls "
-                         "inside (falls back to 'segments' where the capture is refused); 'segments' = the "
-                         "compute between eager collectives")
+                         "0: 2 with the whole-step graph over RCCL (tools/shard_sim.py, world 8 with stand-in "
+                         "exchanges: 151 us vs 175 us with 1), else 1 (per-segment launches make 2 launch-bound: "
+                         "198 us vs 162 us; DESIGN.md §6)")
+    ap.add_argument("--shard-graph", choices=["full", "segments"], default="full",
+                    help="multi-GPU graph form: 'full' (default) = one hipGraph per step with the RCCL "
+                         "all-to-alls inside (falls back to 'segments' where the capture is refused, e.g. gloo); "
+                         "'segments' = the compute between eager collectives")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -71,6 +73,9 @@ def parse():
     ap.add_argument("--nbatch", type=int, default=NBATCH, help="distinct index batches cycled")
     ap.add_argument("--sustain", type=float, default=2.0,
                     help="seconds of back-to-back steps timed after the K-step region (reported as 'sustained')")
+    ap.add_argument("--probe-region", default="",
+                    help="comma-separated step counts: print the timed region's ms per step for each (graph "
+                         "launch overhead vs K) and exit")
     ap.add_argument("--pipeline", type=int, default=-1,
                     help="where the step's indexer is built: 0 in the forward's launch; 2 inside the previous "
                          "step's apply launch, so the forward only gathers (step API, batches <= 2048); 1 the next "
@@ -324,8 +329,9 @@ def main():
                 engine.step(x, packs[k % nb], dout)
     else:
         from dlrm_jl_amd.sharded import make_bench_engine
-        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb,
-                                                         micro=a.micro or None)
+        full_graph = a.mode == "graph" and a.shard_graph == "full" and dist.get_backend() == "nccl"
+        micro = a.micro or (2 if full_graph and B % 2 == 0 else 1)
+        engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb, micro=micro)
         if a.mode == "graph":
             # each whole step (both all-to-alls included) replayed as one hipGraph; where the
             # backend refuses the capture, the compute between eager collectives
@@ -389,9 +395,10 @@ def main():
             out.append(((k % nb), n - k))
         return out
 
+    probe = [int(v) for v in a.probe_region.split(",") if v]
     if a.mode == "graph":
         try:
-            for piece in set(plan(a.steps)) | set(plan(nb)) | set(plan(a.warmup)):
+            for piece in set(plan(a.steps)) | set(plan(nb)) | set(plan(a.warmup)) | {p for n in probe for p in plan(n)}:
                 if piece not in graphs:
                     graphs[piece] = capture(*piece)
             torch.cuda.synchronize()
@@ -435,6 +442,14 @@ def main():
             ms = float(tt.item())
         return ms
 
+    if probe:
+        res = {}
+        for rep in range(3):
+            for n in probe:
+                res.setdefault(n, []).append(round(timed(n), 5))
+        if rank == 0:
+            print(json.dumps({"probe_region_ms_per_step": {n: v for n, v in res.items()}}))
+        return
     ms = timed(a.steps)
     # sustained: >= a.sustain seconds of back-to-back steps (whole cycles over the nb batches), so a
     # short K does not hide clock ramp or cache effects; reported beside value, not instead of it
@@ -706,6 +721,9 @@ def main():
         }
         print(json.dumps(line))
     if world > 1:
+        # captured graphs hold RCCL work and keep a reference on the communicator: release them
+        # first, or destroying the process group waits on them forever
+        engine.close()
         dist.destroy_process_group()
 
 

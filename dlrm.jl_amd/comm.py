@@ -41,6 +41,17 @@ class CommExchange:
         with torch.cuda.device(self.ctx.device):
             self.ctx.check(self.lib.dlrm_comm_init(self.ctx.bind(), self._uid, self.rank, self.world, ctypes.byref(h)))
         self.handle = h
+        # hipGraphs that captured this communicator's exchanges.  RCCL keeps a reference on the
+        # communicator for every live graph holding its work, and ncclCommDestroy waits for those
+        # references to go: destroying the communicator while such a graph is alive never returns
+        # (the round-4 "capture hang" of test_sharded_whole_step_graph_world1 was exactly that, at
+        # the test's end, when Python freed the communicator before the engine's graphs).  So the
+        # graphs are registered here and reset before the communicator is destroyed.
+        self._graphs = []
+
+    def retain_graphs(self, graphs):
+        """Registers captured graphs that hold this communicator's work (reset by close())."""
+        self._graphs.extend(graphs)
 
     @staticmethod
     def _counts(counts):
@@ -59,7 +70,11 @@ class CommExchange:
                                                   self._counts(counts), ptr(gsend), ptr(grecv)))
 
     def close(self):
+        for g in getattr(self, "_graphs", ()):
+            g.reset()  # (first: see __init__)
+        self._graphs = []
         if getattr(self, "handle", None):
+            torch.cuda.synchronize(self.ctx.device)
             self.lib.dlrm_comm_destroy(self.handle)
             self.handle = None
 

@@ -47,11 +47,15 @@ mutable struct Context
     # Descent η of the update! that follows (lets the pullback step the once-hit rows itself)
     fused::Bool
     lr::Union{Nothing,Float32}
-    function Context(device::Integer; stream::Ptr{Cvoid} = C_NULL, fused::Bool = false, lr = nothing)
+    # defer_update (fused, lr known): update! leaves its apply launch to the next maplookup, which runs
+    # it with that batch's indexer build -- no host synchronisation per step (bounds: see poll_bounds!)
+    defer::Bool
+    function Context(device::Integer; stream::Ptr{Cvoid} = C_NULL, fused::Bool = false, lr = nothing,
+                     defer_update::Bool = true)
         out = Ref{Ptr{Cvoid}}(C_NULL)
         rc = ccall((:dlrm_ctx_create, libdlrm), Cint, (Cint, Ptr{Cvoid}, Ref{Ptr{Cvoid}}), device, stream, out)
         rc == 0 || throw(DLRMError(rc, "dlrm_ctx_create"))
-        ctx = new(out[], fused, lr === nothing ? nothing : Float32(lr))
+        ctx = new(out[], fused, lr === nothing ? nothing : Float32(lr), defer_update)
         finalizer(c -> ccall((:dlrm_ctx_destroy, libdlrm), Cint, (Ptr{Cvoid},), c.ptr), ctx)
         return ctx
     end
@@ -67,6 +71,14 @@ end
 
 synchronize(ctx::Context) = check(ctx, ccall((:dlrm_sync, libdlrm), Cint, (Ptr{Cvoid},), ctx.ptr))
 check_bounds(ctx::Context) = check(ctx, ccall((:dlrm_check_bounds, libdlrm), Cint, (Ptr{Cvoid},), ctx.ptr))
+# the last copy of the device bounds flag that has reached host memory (no GPU call; the step
+# backward stores it, dlrm_error_snapshot queues one)
+function error_peek(ctx::Context)
+    w = Ref{Cuint}(0)
+    check(ctx, ccall((:dlrm_error_peek, libdlrm), Cint, (Ptr{Cvoid}, Ref{Cuint}), ctx.ptr, w))
+    return w[]
+end
+error_snapshot(ctx::Context) = check(ctx, ccall((:dlrm_error_snapshot, libdlrm), Cint, (Ptr{Cvoid},), ctx.ptr))
 
 #####
 ##### Device buffers owned from Julia (dlrm_malloc / dlrm_free / dlrm_memcpy_*)
@@ -467,6 +479,11 @@ end
 # its pullback dlrm_step_bwd(DLRM_STEP_BWD_ONLY) (once-hit rows stepped with η there; without lr,
 # dlrm_interact_bwd_gather writes every dt row), and update! the apply launch.  Results are those of
 # the five-launch chain above, bit for bit (tests/test_gpu_parity.py, through the same ABI).
+# With lr known and `defer_update` (the Context default), update! returns at once and the next
+# maplookup runs its apply launch together with that batch's indexer build (flush!), so the next
+# forward only gathers and no call synchronises: out-of-range indices surface as BoundsError at a
+# later maplookup (poll_bounds!, from the flag the step backward copies to host memory) or at
+# check_bounds(tables), with no row of the failing step written (Python mirror: HipTables).
 
 const STEP_BWD_ONLY, STEP_APPLY_ONLY, UPDATE_PREBUILT = Cuint(1), Cuint(2), Cuint(2)
 
@@ -491,15 +508,89 @@ chain_step(tables, B::Int) =
     get!(() -> HipTrainStep(first(tables).data.ctx, tables, B; lr = something(first(tables).data.ctx.lr, 0f0)),
          get!(() -> Dict{Int,Any}(), CHAIN_STEPS, tables), B)
 
+# Deferred update!: tables => the HipTrainStep whose apply launch the next maplookup runs, and the
+# table sets with deferred steps whose bounds flag has not been checked yet.
+const CHAIN_PENDING = IdDict{Any,Any}()
+const CHAIN_UNCHECKED = IdDict{Any,Bool}()
+
+"""
+    flush!(tables; next = nothing)
+
+Runs a deferred `update!`'s apply launch.  With `next` (the next maplookup's `PackedIndices`, same
+batch size) the same launch builds their split indexer (dlrm_step_bwd_prepare), so the next
+forward only gathers.  The step stays pending if the call fails.
+"""
+function flush!(tables; next = nothing)
+    st = get(CHAIN_PENDING, tables, nothing)
+    st === nothing && return nothing
+    ctx = st.ctx
+    d, B = size(st.x)
+    if next !== nothing && next.batch == st.idx.batch && next.lookups == 1
+        nix = st.spare === nothing ? HipIndexer(ctx, length(st.tables), B) : st.spare
+        check(ctx, ccall((:dlrm_step_bwd_prepare, libdlrm), Cint,
+                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid},
+                          Int64, Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat,
+                          Ptr{Cvoid}, Ptr{Cvoid}, Cuint),
+                         ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
+                         st.x.ptr, d, st.delta.ptr, size(st.delta, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                         size(st.dt, 1), ctx.lr, nix.ptr, next.data.ptr, STEP_APPLY_ONLY))
+        st.spare, st.ix = st.ix, nix
+        st.pending = next => next          # train_step_fwd! finds this batch's indexer prepared
+    else
+        check(ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
+                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,
+                          Ptr{Cvoid}, Int64, Cint, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Cfloat, Cuint),
+                         ctx.ptr, tableset(st.tables), st.ix.ptr, st.idx.data.ptr, DLRM_I32, st.idx.batch, 1, B,
+                         st.x.ptr, d, st.delta.ptr, size(st.delta, 1), st.padding, st.dx.ptr, d, st.dt.ptr,
+                         size(st.dt, 1), ctx.lr, STEP_APPLY_ONLY))
+    end
+    delete!(CHAIN_PENDING, tables)
+    return nothing
+end
+
+"""
+    poll_bounds!(tables)
+
+No GPU call: throws `BoundsError` if a deferred step had an out-of-range index, as far as the copy of
+the device flag that has reached host memory shows (the step backward stores it).  Every kernel
+skips its table writes once the flag is set, so the tables hold the state before the failing step;
+the pending apply of that step is dropped.
+"""
+function poll_bounds!(tables)
+    get(CHAIN_UNCHECKED, tables, false) || return nothing
+    ctx = first(tables).data.ctx
+    error_peek(ctx) == 0 && return nothing
+    delete!(CHAIN_PENDING, tables)
+    delete!(CHAIN_UNCHECKED, tables)
+    check_bounds(ctx)                     # synchronises, clears the flag, throws BoundsError
+    return nothing
+end
+
+"""
+    check_bounds(tables::AbstractVector{<:HipEmbedding})
+
+A host-visible point for a table set trained through the deferred chain: runs a pending update,
+synchronises and throws `BoundsError` if any step since the last check had an out-of-range index.
+Call it before reading the tables back (e.g. `Array(tables[t].data)`).
+"""
+function check_bounds(tables::AbstractVector{<:HipEmbedding})
+    flush!(tables)
+    delete!(CHAIN_UNCHECKED, tables)
+    check_bounds(first(tables).data.ctx)
+end
+
 function _fused_maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse, P::Integer) where {D,T}
     ctx = first(tables).data.ctx
     idx = sparse isa PackedIndices ? sparse : pack(ctx, sparse)
+    poll_bounds!(tables)                  # a deferred step's BoundsError (no GPU call)
+    flush!(tables; next = idx)            # its apply launch, with this batch's indexer build
     return HipLookup{T}(tables, idx, Int(P))
 end
 
 function _fused_interact(dot::HipDotInteraction, x::AbstractMatrix{T}, ys::HipLookup{T}) where {T}
     d, B = size(x)
     d == ys.P || throw(DimensionMismatch("x has $d rows, maplookup reserved $(ys.P)"))
+    flush!(ys.tables)                     # (an update! deferred after this lookup was made runs first)
     st = chain_step(ys.tables, B)
     train_step_fwd!(st, x isa DeviceMatrix ? x : Matrix{T}(x), ys.idx)   # dlrm_step_fwd
     st.bwd = :none
@@ -561,7 +652,15 @@ end
 function _fused_update!(opt, st, tables)
     ctx = st.ctx
     d, B = size(st.x)
-    if st.bwd === :once_hit_applied
+    if st.bwd === :once_hit_applied && ctx.defer
+        opt.eta == ctx.lr || throw(ArgumentError("the pullback stepped the once-hit rows with η = $(ctx.lr), update! got $(opt.eta)"))
+        # the apply launch runs in the next maplookup (flush!); bounds surface there (poll_bounds!)
+        # or at check_bounds(tables): no host synchronisation here
+        CHAIN_PENDING[tables] = st
+        CHAIN_UNCHECKED[tables] = true
+        st.bwd = :done
+        return nothing
+    elseif st.bwd === :once_hit_applied
         opt.eta == ctx.lr || throw(ArgumentError("the pullback stepped the once-hit rows with η = $(ctx.lr), update! got $(opt.eta)"))
         check(ctx, ccall((:dlrm_step_bwd, libdlrm), Cint,
                          (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Ptr{Cvoid}, Int64,

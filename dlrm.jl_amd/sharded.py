@@ -41,8 +41,10 @@ or, in the CPU gloo tests, a test-only CPU checker.  torch.distributed (backend 
 = RCCL over xGMI on MI355X) carries the two all-to-alls (uneven table counts per rank: the
 split-size form of all_to_all_single), or, with exchange="abi", the library's own RCCL
 communicator (dlrm_alltoall_fwd / _bwd, dlrm.jl_amd/comm.py).  The bench replays each whole step,
-collectives included, as one hipGraph (`capture_full`); where the backend's collectives cannot be
-captured, the compute between them (`capture`) with the collectives launched eagerly.
+collectives included, as one hipGraph (`capture_full`, `--shard-graph full`, the default); where the
+backend's collectives cannot be captured (gloo), the compute between them (`capture`) with the
+collectives launched eagerly.  A graph holding RCCL work keeps a reference on its communicator, so
+`close()` (graphs first, then the communicator) must run before the communicator is destroyed.
 """
 import os
 
@@ -452,15 +454,38 @@ class ShardedHotPath:
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(s)
         self._full = graphs
+        if self.comm is not None:
+            self.comm.retain_graphs(graphs)
+
+    def release_graphs(self):
+        """Drops every captured graph.  A graph holding RCCL work keeps a reference on its
+        communicator, and destroying the communicator (dist.destroy_process_group(), or the library
+        communicator's close) waits for that reference: release the graphs first (close() does)."""
+        for g in (self._full or []):
+            g.reset()
+        if self._graphs is not None:
+            look, mid, upd, ixg = self._graphs
+            for g in [g for gs in look for g in gs] + mid + upd + ixg:
+                g.reset()
+        self._full = self._graphs = None
+
+    def close(self):
+        """Releases the graphs, then the library communicator (exchange="abi").  Call before
+        dist.destroy_process_group() when the step was captured with the torch exchange."""
+        self.release_graphs()
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
 
 
 def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, capacity=None, nbatch=8,
                       micro=None):
     """Bench setup for one rank: local tables (full size) and nbatch index batches for the
     global batch; returns (engine, step(k) closure, prepare_graphs() closure).  batch_local =
-    global batch / world for strong scaling.  micro: micro-batches per step (default 1: with two,
-    the per-micro-batch launches and cross-stream event hops cost more than the exchange overlap
-    hides -- tools/shard_sim.py at world 8: 185 us per step, launch-bound, against 103 us with one)."""
+    global batch / world for strong scaling.  micro: micro-batches per step (default 1; bench.py
+    takes 2 with the whole-step graph, where the overlap pays -- tools/shard_sim.py at world 8 with
+    stand-in exchanges: 151 us vs 175 us -- and 1 with per-segment graphs, where two micro-batches
+    are launch-bound: 198 us vs 162 us)."""
     import numpy as np
     if micro is None:
         micro = 1
@@ -497,6 +522,7 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
     x = torch.randn((batch_local, D), device=device, generator=g).to(dt)
     dout = (torch.randn((batch_local, eng.width), device=device, generator=g) * 1e-3).to(dt)
     eng.bench_packs = packs  # the index batches (tools/bench_full_step.py drives the full step with them)
+    eng._bench_x, eng._bench_dout = x, dout
 
     def step(k):
         if eng._graphs is not None or eng._full is not None:

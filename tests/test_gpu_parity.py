@@ -1239,17 +1239,15 @@ def test_comm_abi_world1_exchange_and_sharded_step(pkg, gpu):
         assert torch.equal(a.data, b.data)
 
 
-@pytest.mark.parametrize("exchange", [
-    pytest.param("abi", marks=pytest.mark.skip(reason="the library communicator's one-rank self send/recv did not "
-                                               "return inside stream capture (r10, 1-GPU box); not run")),
-    pytest.param("torch", marks=pytest.mark.skip(reason="torch.distributed 'nccl' all_to_all_single inside "
-                                                 "stream capture on a one-rank group did not return within 120 s "
-                                                 "(r11, 1-GPU box); not run"))])
-def test_sharded_whole_step_graph_world1(pkg, gpu, exchange):
+@pytest.mark.timeout(90)
+@pytest.mark.parametrize("exchange,micro", [("abi", 1), ("torch", 1), ("abi", 2), ("torch", 2)])
+def test_sharded_whole_step_graph_world1(pkg, gpu, exchange, micro):
     """capture_full: the whole sharded step -- side-stream index build, lookup, both all-to-alls
     (the library's RCCL communicator, or torch.distributed "nccl" = RCCL), interaction, update --
-    captured as one hipGraph per index batch on a one-rank communicator, replayed, equals the
-    eager step bit for bit (tables, out, dx) over the same sequence of batches."""
+    captured as one hipGraph per index batch on a one-rank communicator (micro = 2: the exchanges
+    on the comm stream, overlapping the other micro-batch's compute), replayed, equals the eager
+    step bit for bit (tables, out, dx) over the same sequence of batches; close() then releases the
+    graphs before the communicators (the order RCCL needs)."""
     import socket
     import torch.distributed as dist
     from dlrm_jl_amd.sharded import HipShardOps, ShardedHotPath, TablePartition
@@ -1274,7 +1272,8 @@ def test_sharded_whole_step_graph_world1(pkg, gpu, exchange):
 
         def engine():
             ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
-            return ops, ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=exchange)
+            return ops, ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=exchange,
+                                       micro=micro)
         ops_e, eng_e = engine()
         for k in (0, 1, 0):
             eng_e.step(x, idxs[k], dout)
@@ -1289,6 +1288,10 @@ def test_sharded_whole_step_graph_world1(pkg, gpu, exchange):
         assert torch.equal(eng_g.out, eng_e.out) and torch.equal(eng_g.dx, eng_e.dx)
         for a, b in zip(ops_g.ts, ops_e.ts):
             assert torch.equal(a.data, b.data)
+        # the graphs hold RCCL work: released before their communicator is destroyed (round 4's hang
+        # was ncclCommDestroy at this test's end, waiting on graphs that were still alive)
+        eng_g.close()
+        eng_e.close()
     finally:
         if own_pg:
             dist.destroy_process_group()
