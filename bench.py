@@ -47,9 +47,9 @@ def parse():
                          "weak scaling, the workload's batch per GPU")
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
-                         "0: 2 with the whole-step graph over RCCL (tools/shard_sim.py, world 8 with stand-in "
-                         "exchanges: 151 us vs 175 us with 1), else 1 (per-segment launches make 2 launch-bound: "
-                         "198 us vs 162 us; DESIGN.md §6)")
+                         "0: 1 -- with the whole step in one graph, a replay runs its parallel branches largely in "
+                         "series on this stack, so 2 measured 167 us against 157 us (tools/shard_sim.py, world 8, "
+                         "stand-in exchanges; DESIGN.md §6)")
     ap.add_argument("--shard-graph", choices=["full", "segments"], default="full",
                     help="multi-GPU graph form: 'full' (default) = one hipGraph per step with the RCCL "
                          "all-to-alls inside (falls back to 'segments' where the capture is refused, e.g. gloo); "
@@ -216,11 +216,19 @@ def cpu_baseline(pkg, w, seconds, threads):
 
 
 def measured_ceiling(dev, row_bytes):
-    """The HBM rates this box reaches, measured here beside the 8 TB/s spec (report both):
-    a 1 GiB device-to-device copy (read + write) and a gather of 262,144 random rows of `row_bytes`
-    from a 4 GiB buffer into a dense output (torch.index_select; read + write), each the best of 5
-    timed runs after a warm-up, on the current stream with HIP events.  tools/fetch_probe.hip is the
-    same measurement with PMC traffic (profiles/r6r_fetch_probe.json)."""
+    """The HBM rates this box reaches with hand-written gfx950 kernels (tools/bw_probe.hip, built
+    into dlrm.jl_amd/lib/libdlrm_probe.so), beside the 8 TB/s spec (report both): a
+    1 GiB nontemporal copy (read + write), a 1 GiB read, and reads of 262,144 random line-aligned rows
+    of 512 B, of this workload's row size and of 64 B from a 4 GiB buffer (tools/fetch_probe.hip's
+    shape) -- each the best of 5 HIP-event-timed launches on the current stream after a warm-up."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "dlrm.jl_amd", "lib", "libdlrm_probe.so"))
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    lib.dlrm_probe_copy.argtypes = [vp, vp, i64, vp]
+    lib.dlrm_probe_read.argtypes = [vp, i64, vp, vp]
+    lib.dlrm_probe_gather.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, vp, vp]
+    st = vp(torch.cuda.current_stream(dev).cuda_stream)
+
     def best(fn, nbytes, reps=5):
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -234,19 +242,25 @@ def measured_ceiling(dev, row_bytes):
         return round(nbytes / min(t) / 1e9, 1)
     out = {}
     try:
-        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        n = 1 << 30
+        src = torch.empty(n // 4, dtype=torch.float32, device=dev).fill_(1.0)
         dst = torch.empty_like(src)
-        out["stream_copy_GBps"] = best(lambda: dst.copy_(src), 2 * src.numel() * 4)
+        sink = torch.empty(1 << 20, dtype=torch.float32, device=dev)
+        p = lambda t: vp(t.data_ptr())  # noqa: E731
+        out["stream_copy_GBps"] = best(lambda: lib.dlrm_probe_copy(p(src), p(dst), n, st), 2 * n)
+        out["stream_read_GBps"] = best(lambda: lib.dlrm_probe_read(p(src), n, p(sink), st), n)
         del src, dst
-        cols = max(1, row_bytes // 4)
-        big = torch.empty((1 << 30) // cols, cols, dtype=torch.float32, device=dev)
-        idx = torch.randint(0, big.shape[0], (262144,), device=dev)
-        res = torch.empty((262144, cols), dtype=torch.float32, device=dev)
-        out["gather_GBps"] = best(lambda: torch.index_select(big, 0, idx, out=res), 2 * res.numel() * 4)
-        out["gather_row_bytes"] = cols * 4
-        out["method"] = ("best of 5 HIP-event-timed runs: 1 GiB copy (read+write); torch.index_select of 262,144 "
-                         "random rows from 4 GiB (read+write)")
-        del big, idx, res
+        big = torch.empty((4 << 30) // 4, dtype=torch.float32, device=dev).fill_(1.0)
+        rows = 262144
+        for rb in sorted({512, int(row_bytes), 64}):
+            if rb in (64, 128, 256, 512, 1024):
+                out[f"gather_{rb}B_GBps"] = best(lambda: lib.dlrm_probe_gather(p(big), 4 << 30, rb, rows, p(sink), st),
+                                                 rows * rb)
+        out["gather_GBps"] = out.get(f"gather_{int(row_bytes)}B_GBps")
+        out["gather_row_bytes"] = int(row_bytes)
+        out["method"] = ("tools/bw_probe.hip, best of 5 HIP-event-timed launches: 1 GiB nontemporal copy "
+                         "(read+write bytes), 1 GiB read, 262,144 random line-aligned rows read from 4 GiB")
+        del big
         torch.cuda.empty_cache()
     except Exception as e:  # (memory / API trouble: reported, never fatal)
         out["error"] = repr(e)
@@ -329,8 +343,7 @@ def main():
                 engine.step(x, packs[k % nb], dout)
     else:
         from dlrm_jl_amd.sharded import make_bench_engine
-        full_graph = a.mode == "graph" and a.shard_graph == "full" and dist.get_backend() == "nccl"
-        micro = a.micro or (2 if full_graph and B % 2 == 0 else 1)
+        micro = a.micro or 1
         engine, step, prepare_graphs = make_bench_engine(pkg, w, B, dev, rank, world, a.lr, nbatch=nb, micro=micro)
         if a.mode == "graph":
             # each whole step (both all-to-alls included) replayed as one hipGraph; where the
@@ -653,12 +666,23 @@ def main():
         ach = stages[dom]["GBps"]
         step_bytes = sum(bytes_[n] for n in names)  # every launch of one step (side-stream work included)
         step_gbs = step_bytes / (ms * 1e-3) / 1e9
+        # SURVEY.md §8(d)'s un-fused per-sample bytes (BASELINE.md's denominator: 112.6 KB/sample at the
+        # metric config): per (sample, table) the gather L*I + L*D*E + D*E and the scatter-SGD
+        # D*E + L*I + 2*D*E (U = B, no dedupe), plus the interaction's fwd F*D*E + (d+P)*E and bwd
+        # (d+P)*E + 2*F*D*E + d*E
+        Fu, Pu = T + 1, (T + 1) * T // 2
+        unfused = B * (T * (2 * L * 4 + L * D * E + 4 * D * E) + Fu * D * E + (D + Pu) * E
+                       + (D + Pu) * E + 2 * Fu * D * E + D * E)
+        unf_gbs = unfused / (ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": (prof or {}).get(dom, {}).get("hbm_bytes_per_launch"),
                     "alg_bytes_per_launch": int(bytes_[dom]), "avg_launch_us": stages[dom]["us"],
                     "step": {"alg_bytes": int(step_bytes), "ms": round(ms, 4), "GBps": round(step_gbs, 1),
-                             "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
+                             "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                             "bytes_basis": "fused: the algorithmic bytes of this step's own launches (frac); "
+                                            "frac_unfused: SURVEY §8(d)'s un-fused per-sample bytes (BASELINE.md)",
+                             "unfused_bytes": int(unfused), "frac_unfused": round(unf_gbs / HBM_PEAK_GBS, 4)},
                     "stages": stages}
         if a.ceiling:
             roofline["measured_ceiling"] = measured_ceiling(dev, D * E)
@@ -670,6 +694,13 @@ def main():
                                    "dominant_by": "rocprofv3 avg duration" if have else "HIP events",
                                    "rocprof_avg_us": {n: round(prof[n]["avg_us"], 2) for n in names
                                                       if n in prof and "avg_us" in prof[n]}}
+            # PMC HBM traffic (2 FETCH_SIZE + WRITE_SIZE per launch) beside each stage's algorithmic bytes:
+            # a stage whose frac counts cache re-reads (pooled Zipf rows) shows traffic well below them
+            for n in names:
+                tb = prof.get(n, {}).get("hbm_bytes_per_launch")
+                if tb:
+                    stages[n]["traffic"] = int(tb)
+                    stages[n]["traffic_GBps"] = round(tb / (stages[n]["us"] * 1e-6) / 1e9, 1)
             mf = {n: round(prof[n]["mfma_busy"], 4) for n in names if n in prof and "mfma_busy" in prof[n]}
             if mf:  # north_star: MFMA utilisation of the interaction kernels (SIMD-cycle fraction)
                 roofline["mfma"] = mf

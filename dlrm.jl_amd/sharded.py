@@ -382,21 +382,30 @@ class ShardedHotPath:
             main.wait_event(self._ix_done)
             update()
             return
+        # M > 1: every exchange on the step's own stream (the capture's origin stream under graph
+        # capture), the compute that overlaps them on the second stream.  (The other way round --
+        # exchanges on the second stream -- captured fine but segfaulted in graph instantiation,
+        # for the library's and torch's RCCL exchange alike: tools/capture_diag.py)
+        #   main: lookup(0) | a2a_fwd(0) | a2a_fwd(1) ... | a2a_bwd(0) ... | update
+        #   cs  :   lookup(1..M-1) | interact(0) | interact(1) ...
+        lookup(0)
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            for m in range(1, M):
+                lookup(m)
+                ev_look[m].record(cs)
         for m in range(M):
-            lookup(m)
-            ev_look[m].record(main)
-            cs.wait_event(ev_look[m])
+            if m:
+                main.wait_event(ev_look[m])
+            self.exchange_fwd(m)
+            ev_recv[m].record(main)
+            cs.wait_event(ev_recv[m])
             with torch.cuda.stream(cs):
-                self.exchange_fwd(m)
-                ev_recv[m].record(cs)
+                interact(m)
+                ev_bwd[m].record(cs)
         for m in range(M):
-            main.wait_event(ev_recv[m])
-            interact(m)
-            ev_bwd[m].record(main)
-            cs.wait_event(ev_bwd[m])
-            with torch.cuda.stream(cs):
-                self.exchange_bwd(m)
-        main.wait_stream(cs)
+            main.wait_event(ev_bwd[m])
+            self.exchange_bwd(m)
         main.wait_event(self._ix_done)
         update()
 
@@ -482,10 +491,10 @@ def make_bench_engine(pkg, w, batch_local, device, rank, world, lr, seed=51234, 
                       micro=None):
     """Bench setup for one rank: local tables (full size) and nbatch index batches for the
     global batch; returns (engine, step(k) closure, prepare_graphs() closure).  batch_local =
-    global batch / world for strong scaling.  micro: micro-batches per step (default 1; bench.py
-    takes 2 with the whole-step graph, where the overlap pays -- tools/shard_sim.py at world 8 with
-    stand-in exchanges: 151 us vs 175 us -- and 1 with per-segment graphs, where two micro-batches
-    are launch-bound: 198 us vs 162 us)."""
+    global batch / world for strong scaling.  micro: micro-batches per step (default 1: with the
+    whole step in one graph a replay runs the parallel branches largely in series on this stack --
+    tools/shard_sim.py at world 8 with stand-in exchanges: 167 us with 2 against 157 us with 1 --
+    and with per-segment graphs two micro-batches are launch-bound: 198 us vs 162 us)."""
     import numpy as np
     if micro is None:
         micro = 1

@@ -283,3 +283,61 @@ def test_terabyte_bf16_full_size(pkg, gpu):
         assert torch.equal(tables[t][u].float(), (-ref).float().to(torch.bfloat16).float())
         nz = (tables[t] != 0).any(dim=1).nonzero().flatten()
         assert torch.isin(nz, u).all(), "a row no index touched was written"
+
+
+@pytest.mark.parametrize("rank", [5, 0])
+def test_terabyte_fp32_shard_of_world8(pkg, gpu, rank):
+    """configs[3] in its own form: fp32 Criteo-Terabyte tables sharded by table over 8 GPUs, global
+    batch 2048 (256 per GPU).  On this one GPU, rank `rank`'s shard at full size (rank 5: the
+    292.8M-row table, 150 GB fp32; rank 0: 116 GB) runs its table-owning half of the sharded step --
+    the lookup of its tables for all 2048 samples straight into the exchange's send layout, the split
+    indexer over the global batch, and the update from the received gradient rows -- checked against
+    a host gather and the closed-form scatter-add on the touched rows (integer gradients on zeroed
+    tables: exact), and no untouched row written."""
+    from dlrm_jl_amd.sharded import HipShardOps, TablePartition
+    rows = pkg.TERABYTE_EMBEDDING_SIZES
+    world, Bg, D = 8, 2048, 128
+    B = Bg // world
+    part = TablePartition.fitting(rows, world, D * 4, int(260e9))
+    mine = part.tables(rank)
+    need = sum(rows[t] for t in mine) * D * 4
+    if torch.cuda.get_device_properties(gpu).total_memory < need + 30e9:
+        pytest.skip("needs a 288 GB MI355X")
+    Tr = len(mine)
+    # row-encoded fp32 tables: columns 0..2 = the row's three 11-bit pieces (exact in fp32), 3 = table
+    tables = [torch.empty((rows[t], D), dtype=torch.float32, device=gpu) for t in mine]
+    chunk = 1 << 24
+    for k, (t, tab) in enumerate(zip(mine, tables)):
+        tab[:, 4:] = 0.5
+        for r0 in range(0, rows[t], chunk):
+            r = torch.arange(r0, min(rows[t], r0 + chunk), device=gpu, dtype=torch.int64)
+            for q in range(3):
+                tab[r0:r0 + len(r), q] = ((r >> (11 * q)) & 2047).to(torch.float32)
+            tab[r0:r0 + len(r), 3] = float(t)
+    rng = np.random.default_rng(50 + rank)
+    perms = [pkg.zipf_perm(rng, rows[t]) for t in mine]
+    idx_np = np.stack([pkg.zipf_rows(rng, rows[t], Bg, 1.05, p) for t, p in zip(mine, perms)]).astype(np.int32)
+    idx = torch.from_numpy(idx_np).to(gpu)
+    ops = HipShardOps(tables, Bg, 1, 1.0, device=gpu)
+    p = pkg.PackedIndices(idx.reshape(Tr, Bg, 1))
+    send = torch.empty((world * Tr * B * D,), dtype=torch.float32, device=gpu)
+    ops.lookup_blocked(p, send, D, B * D, B, Tr * B * D)
+    got = send.view(world, Tr, B, D).permute(1, 0, 2, 3).reshape(Tr, Bg, D)
+    dec = sum(got[:, :, q].to(torch.int64) << (11 * q) for q in range(3))
+    assert torch.equal(dec, idx.to(torch.int64))
+    assert torch.equal(got[:, :, 3], torch.tensor(mine, device=gpu, dtype=torch.float32)[:, None].expand(Tr, Bg))
+    del send, got
+    for tab in tables:
+        tab.zero_()
+    ops.build_indexer(p)
+    gi = torch.from_numpy(rng.integers(-4, 5, size=(Bg, Tr * D)).astype(np.float32)).to(gpu)
+    ops.update(p, gi, prebuilt=True)
+    ops.check_bounds()
+    for k, t in enumerate(mine):
+        rows_t = idx[k].long()
+        u = torch.unique(rows_t)
+        ref = torch.zeros((len(u), D), dtype=torch.float64, device=gpu)
+        ref.index_add_(0, torch.searchsorted(u, rows_t), gi[:, k * D:(k + 1) * D].double())
+        assert torch.equal(tables[k][u], (-ref).float()), (rank, t)
+        nz = (tables[k] != 0).any(dim=1).nonzero().flatten()
+        assert torch.isin(nz, u).all(), "a row no index touched was written"

@@ -6,7 +6,7 @@ before and after every host call, so the log shows whether the host blocks insid
 
     python tools/capture_diag.py OUTDIR variant[,variant...]
 
-variants: abi-eager, abi-op[:mode], torch-op[:mode], abi-step[:mode], torch-step[:mode]
+variants: abi-eager, abi-op[:mode], torch-op[:mode], abi-step[:mode], torch-step[:mode], abi-step2, torch-step2
 (mode = torch.cuda.graph capture_error_mode: global (default) | thread_local | relaxed)
 """
 import faulthandler
@@ -95,10 +95,62 @@ def child(variant):
     F = T + 1
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
     ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
-    eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind)
-    eng.step(x, idx, dout)
-    torch.cuda.synchronize()
-    mark("eager step ok")
+    micro = 2 if what == "step2" else 1
+    if what != "step2m":
+        eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind, micro=micro)
+        eng.step(x, idx, dout)
+        torch.cuda.synchronize()
+        mark("eager step ok")
+    if what == "step2m":  # M = 2 schedule written out, a marker after every host call
+        eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind, micro=2)
+        eng.step(x, idx, dout)
+        torch.cuda.synchronize()
+        mark("eager M=2 step ok")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            g.capture_begin(capture_error_mode=mode)
+            main, cs = torch.cuda.current_stream(), eng._cstream
+            ev_look, ev_recv, ev_bwd, _ = eng._ev
+            for m in range(2):
+                eng.seg_lookup(idx, m)
+                ev_look[m].record(main)
+                cs.wait_event(ev_look[m])
+                with torch.cuda.stream(cs):
+                    mark(f"in capture: exchange_fwd({m}) on the comm stream")
+                    eng.exchange_fwd(m)
+                    mark(f"in capture: exchange_fwd({m}) returned")
+                    ev_recv[m].record(cs)
+            for m in range(2):
+                main.wait_event(ev_recv[m])
+                eng.seg_interact(x, dout, m)
+                ev_bwd[m].record(main)
+                cs.wait_event(ev_bwd[m])
+                with torch.cuda.stream(cs):
+                    mark(f"in capture: exchange_bwd({m})")
+                    eng.exchange_bwd(m)
+                    mark(f"in capture: exchange_bwd({m}) returned")
+            main.wait_stream(cs)
+            eng.seg_update(idx)
+            mark("in capture: all recorded; capture_end")
+            g.capture_end()
+            mark("capture_end returned")
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        mark("replay synced")
+        return
+    if micro > 1:  # the engine's own capture, markers around it
+        mark(f"capture_full (M = {micro}) begin")
+        eng.capture_full(x, [idx], dout)
+        mark("capture_full returned")
+        eng.step_graphed(0)
+        torch.cuda.synchronize()
+        mark("replay synced")
+        eng.close()
+        mark("closed")
+        return
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
