@@ -107,6 +107,17 @@ static int step_parts_log2(int dflt = kStepParts) {
     return p >= 16 ? 4 : (p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0)));
 }
 
+// vshift of the wave build of `batch` positions per table (the step forward's in-launch build and
+// the in-apply / prepared builds): 16 parts per table up to 2048 positions (DLRM_STEP_PARTS may force
+// fewer, >= 4), then 16 parts per 2048 positions (wave_vshift)
+static int wave_parts_log2(int64_t batch) {
+    if (batch > kStepIndexMaxN) return wave_vshift(batch);
+    const int vs = step_parts_log2(kWaveBuildParts);
+    return vs < 2 ? 2 : vs;
+}
+
+static bool has_parts(const dlrm_indexer* ix, int vs) { return (int64_t)ix->TV >= ((int64_t)ix->T << vs) && ix->T > 0; }
+
 static void record_build(dlrm_indexer* ix, bool split, const void* indices, int itype, int64_t tstride, int base,
                          int B, int L) {
     ix->built = true;
@@ -574,11 +585,10 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->T = num_tables;
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
     const int64_t T0 = num_tables > 0 ? num_tables : 1;
-    // the forward launch's indexer (batch <= kStepIndexMaxN) and the parts build (N <= kPartsMaxN)
-    // sort each table as up to kStepMaxParts parts (by the low bits of the row): the per-table
-    // arrays then hold that many virtual tables per table (the hash arrays, single[] and the
-    // global sort scratch stay per real table)
-    const int64_t T = cap <= kPartsMaxN ? kStepMaxParts * T0 : T0;
+    // the wave builds (N <= kWaveMaxN) and the parts build (N <= kPartsMaxN) sort each table as
+    // parts (by the low bits of the row): the per-table arrays then hold indexer_parts(cap) virtual
+    // tables per table (the hash arrays, single[] and the global sort scratch stay per real table)
+    const int64_t T = (int64_t)indexer_parts(cap) * T0;
     ix->TV = (int)T;
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
@@ -590,6 +600,11 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
     const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1)), n0 = (size_t)(T0 * cap);
+    // the wave build's flat item lists: kResLists sub-lists of res_stride records (indexer.hpp), for
+    // the largest build this indexer takes (T / 4 workgroups); the HBM sort scratch for cap > 2048
+    const size_t nrec = T >= 4 ? (size_t)kResLists * (size_t)res_stride((int)(T / 4), cap) + 64 : 64;
+    const int64_t wstride = cap > kStepIndexMaxN && T > T0 ? T * cap + 64 : 0;
+    ix->dev.wstride = wstride;
     Piece pieces[] = {
         {(void**)&ix->dev.keys0, n0 * 4},    {(void**)&ix->dev.keys1, n0 * 4},  {(void**)&ix->dev.vals0, n0 * 4},
         {(void**)&ix->dev.vals1, n0 * 4},    {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
@@ -598,7 +613,8 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
         {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
         {(void**)&ix->prep_err, 16},
-        {(void**)&ix->dev.slice_rec, n * 32}, {(void**)&ix->dev.chunk_rec, n * 32},
+        {(void**)&ix->dev.slice_rec, nrec * 32}, {(void**)&ix->dev.chunk_rec, nrec * 32},
+        {(void**)&ix->dev.wscratch, (size_t)wstride * 5 * 4},
         {(void**)&ix->dev.item_tot, 64},     {(void**)&ix->dev.build_arrive, 2048},
         // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
         {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
@@ -644,7 +660,7 @@ int dlrm_indexer_destroy(dlrm_indexer* ix) {
 static int build_vshift(const dlrm_indexer* ix, int64_t N, bool split) {
     const int p = knobs().build_parts ? knobs().build_parts : (1 << kPartsLog2);
     const int lg = p >= 8 ? 3 : (p >= 4 ? 2 : 1);
-    return split && N > kFastMaxN && N <= kPartsMaxN && ix->TV == kStepMaxParts * ix->T ? lg : 0;
+    return split && N > kFastMaxN && N <= kPartsMaxN && has_parts(ix, lg) ? lg : 0;
 }
 
 int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, const void* indices, int itype,
@@ -691,15 +707,16 @@ int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb,
     if (rc) return rc;
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_prepare: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_prepare: batch %d > capacity %lld", batch, (long long)ix->dev.cap);
-    if (batch > kStepIndexMaxN || tb->T + 1 > 32 || ix->TV != kStepMaxParts * ix->T)
-        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d, %d tables (the step build: batch <= %d, "
-                        "<= 31 tables)", batch, tb->T, kStepIndexMaxN);
+    const int vs = wave_parts_log2(batch);
+    if (batch > kWaveMaxN || tb->T + 1 > 32 || !has_parts(ix, vs))
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d, %d tables (the wave build: batch <= %d, "
+                        "<= 31 tables)", batch, tb->T, kWaveMaxN);
     ix->built = false;
     ix->prepared = false;
-    ix->dev.vshift = step_parts_log2(kWaveBuildParts);
-    if (ix->dev.vshift < 2) ix->dev.vshift = 2;
+    ix->dev.vshift = vs;
+    // (its own launch: bounds errors go to the ctx's flag, as the lookup of the same indices raises them)
     rc = launch_step_prepare(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
-                             ix->prep_err);
+                             ctx->err);
     if (rc) return rc;
     record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
     ix->prepared = true;
@@ -750,9 +767,9 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* ix, int table, int64_t*
     } else {
         // a forward-launch build: merge the table's parts (each sorted by row)
         const int np = 1 << ix->dev.vshift;
-        IndexerTable h[kStepMaxParts];
+        std::vector<IndexerTable> h(np);
         for (int q = 0; q < np && rc == DLRM_OK; ++q) rc = read_indexer_table(ctx, ix, table * np + q, h[q]);
-        size_t k[kStepMaxParts] = {};
+        std::vector<size_t> k(np, 0);
         tt.seg_start.assign(1, 0);
         for (;;) {
             int e = -1;
@@ -851,7 +868,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     ix->prepared = false;
     ix->built = false;
     // the wave build in the forward's launch (vshift >= 2: it also writes the apply's item map)
-    ix->dev.vshift = ix->TV == kStepMaxParts * ix->T ? step_parts_log2(kWaveBuildParts) : 0;
+    ix->dev.vshift = has_parts(ix, wave_parts_log2(kStepIndexMaxN)) ? wave_parts_log2(kStepIndexMaxN) : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev, tb->h_desc.data());
     if (rc == DLRM_OK) {
@@ -984,8 +1001,8 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     // forward's split build (the same parts), so the next dlrm_step_fwd only gathers
     const int NB = (tb->T + 1 + 15) / 16;
     // (the split backward's shapes only: the apply launch that carries the build has no once-hit items)
-    const bool inapply = batch > 0 && tb->T > 0 && batch <= kStepIndexMaxN && NB <= 2 && tb->aligned16 &&
-                         next->TV == kStepMaxParts * next->T &&
+    const bool inapply = batch > 0 && tb->T > 0 && batch <= kWaveMaxN && NB <= 2 && tb->aligned16 &&
+                         has_parts(next, wave_parts_log2(batch)) &&
                          step_split_supported(tb->aligned16, tb->T, tb->dtype, tb->D, x, x_ld);
     if (!inapply)  // no pipelined form for this shape: the plain step (the next forward builds)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
@@ -995,8 +1012,8 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
     next->built = false;
     next->prepared = false;
-    // the wave build: kWaveBuildParts parts per table, one wave each (4 per workgroup: >= 4 parts)
-    next->dev.vshift = step_parts_log2(kWaveBuildParts);
+    // the wave build: 2^wave_parts_log2(batch) parts per table, one wave each (4 per workgroup)
+    next->dev.vshift = wave_parts_log2(batch);
     if (next->dev.vshift < 2) next->dev.vshift = 2;
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
                       next->prep_err};

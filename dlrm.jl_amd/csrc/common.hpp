@@ -227,6 +227,17 @@ constexpr int kFastMaxN = 4096;     // in-LDS indexer (indexer.hpp): positions p
 constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions per table
 constexpr int kStepIndexMaxN = 2048;  // the forward-launch indexer (interact.hip): positions per table
 constexpr int kStepMaxParts = 16;     // ... which sorts a table as up to 16 parts (by the row's low bits)
+// the wave build (indexer.hpp wave_build_group) of the next batch (in the apply launch) or of a
+// prepared batch (dlrm_indexer_prepare): up to kWaveMaxN positions per table, as 16 parts per 2048
+// positions (2^wave_vshift(N) parts per table; a part averages <= 128 positions)
+constexpr int kWaveMaxN = 16384;
+__host__ __device__ constexpr int wave_vshift(int64_t N) {
+    return N <= 2048 ? 4 : (N <= 4096 ? 5 : (N <= 8192 ? 6 : 7));
+}
+// virtual tables per table an indexer of `cap` positions per table provides (its per-part arrays)
+__host__ __device__ constexpr int indexer_parts(int64_t cap) {
+    return cap <= kWaveMaxN ? (1 << wave_vshift(cap)) : 1;
+}
 // the next batch's split build in the apply launch (indexer.hpp wave_build_group): parts per
 // table, one wave each, 4 per workgroup (>= 4)
 #ifndef DLRM_WAVE_PARTS
@@ -282,6 +293,11 @@ struct IndexerDev {
     //   chunk_rec[2c, 2c+1]: the chunk descriptor (write_chunk) with global perm entries
     int4* slice_rec;
     int4* chunk_rec;
+    // the wave build's global sort scratch (cap > kStepIndexMaxN): 5 arrays (K0, V0, K1, V1, R) of
+    // wstride entries, part v's region at v * cap -- for a build workgroup whose four parts overflow
+    // its LDS pool (tiny tables and hot rows at large N), which then sorts in HBM instead
+    uint32_t* wscratch;
+    int64_t wstride;
     int32_t* item_tot;
     uint32_t* build_arrive;  // the reservation words (64 bits, 256 B apart)
     int has_map;

@@ -630,7 +630,9 @@ struct WaveBuildLds {
     int32_t V[2][kStepIndexMaxN + 16];   // positions
     int32_t R[kStepIndexMaxN + 16];      // per-key rank in its digit, then segment starts
     uint32_t cnt[kWaveParts][1 << kWideDigit];  // per-wave digit counters, then digit offsets
-    int tot[kWaveParts][kWaveParts];  // [wave][part]: positions of the workgroup's part q that wave w read
+    // [round][wave][part]: positions of the workgroup's part q that wave w read in round r (a round
+    // = 2048 positions, 512 per wave)
+    int tot[kWaveMaxN / kStepIndexMaxN][kWaveParts][kWaveParts];
 };
 
 // The flat item lists come in kResLists sub-lists: build workgroup g reserves in sub-list g mod 8
@@ -641,7 +643,7 @@ struct WaveBuildLds {
 // at most cap / 2 chunks and as many slices); item_tot[j] / [kResLists + j] = its slices / chunks.
 constexpr int kResSliceShift = 24, kResArriveShift = 44;
 constexpr int kResLists = 8, kResWordStride = 32;  // (u64 words: 256 B apart)
-__device__ __forceinline__ int res_stride(int groups, int64_t cap) {
+__host__ __device__ __forceinline__ int res_stride(int groups, int64_t cap) {
     return ((groups + kResLists - 1) / kResLists) * (int)(cap / 2 + 8);
 }
 // flat record index of item k of the sub-lists with counts cnt[0..kResLists), or -1 past the end
@@ -672,19 +674,34 @@ __device__ __forceinline__ unsigned long long match_digit(uint32_t d, bool ok, i
     return peers;
 }
 
+// The sort's in-wave barrier: LDS parts (the pool) need the wave's LDS operations ordered; a part
+// sorted in HBM (G: the wave build's overflow path) needs its global stores visible to the other
+// lanes of the wave before they read them (workgroup-scope release / acquire).
+template <bool G>
+__device__ __forceinline__ void part_sync() {
+    if constexpr (G) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        wave_lds_sync();
+    }
+}
+
 // One stable counting pass of one wave over keys [0, n) of (Kin, Vin), on the `bits`-bit digit
 // at `shift`, into (Kout, Vout).  Tiles of 64 keys in order; in a tile, the lanes sharing a digit
 // are found by ballots and the group's first lane adds the group's size to the digit's counter
 // with one LDS atomic, whose old value is the group's base (a wave's LDS operations complete in
 // order, so the bases follow the tiles).  Leaves cnt[d] = the start of digit d's bucket; returns
 // the largest bucket.
+template <bool G>
 __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
                                int32_t* Vout, int32_t* R, uint32_t* cnt) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lanes_below();
     const uint32_t dm = (1u << bits) - 1u;
     *(uint4*)&cnt[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
-    wave_lds_sync();
+    wave_lds_sync();  // (cnt: LDS)
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int i = j0 + lane;
         const bool ok = i < n;
@@ -697,7 +714,7 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
         const uint32_t b = (uint32_t)__shfl((int)old, leader, 64);
         if (ok) R[i] = (int)b + rank;
     }
-    wave_lds_sync();
+    part_sync<G>();
     const uint4 c = *(const uint4*)&cnt[4 * lane];  // lane l: digits 4l .. 4l+3
     const int sum = (int)(c.x + c.y + c.z + c.w);
     int o = wave_incl_scan(sum) - sum;
@@ -708,7 +725,7 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
     st.w = o;
     *(uint4*)&cnt[4 * lane] = st;
     const int m = lane63(wave_incl_max((int)max(max(c.x, c.y), max(c.z, c.w))));
-    wave_lds_sync();
+    wave_lds_sync();  // (cnt: LDS)
     for (int j0 = 0; j0 < n; j0 += 64) {
         const int i = j0 + lane;
         if (i < n) {
@@ -718,7 +735,7 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
             Vout[dst] = Vin[i];
         }
     }
-    wave_lds_sync();
+    part_sync<G>();
     return m;
 }
 
@@ -726,6 +743,7 @@ __device__ int wave_count_pass(int n, int shift, int bits, const uint32_t* Kin, 
 // kWideDigit bits (a bucket's keys land in any order; wave_rank_buckets orders them by (key,
 // position)).  Leaves cnt[d] = the start of digit d's bucket; returns the largest bucket (and places
 // nothing when it exceeds kWaveRankMax).
+template <bool G>
 __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_t* Vin, uint32_t* Kout,
                                         int32_t* Vout, int32_t* R, uint32_t* cnt) {
     constexpr uint32_t dm = (1u << kWideDigit) - 1u;
@@ -737,7 +755,7 @@ __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_
     for (int q = 0; q < PL / 4; ++q) c4[q] = make_uint4(0u, 0u, 0u, 0u);
     wave_lds_sync();
     for (int i = lane; i < n; i += 64) R[i] = (int)atomicAdd(&cnt[Kin[i] & dm], 1u);
-    wave_lds_sync();
+    part_sync<G>();
     uint32_t c[PL];
 #pragma unroll
     for (int q = 0; q < PL / 4; ++q) {
@@ -769,12 +787,13 @@ __device__ int wave_count_pass_unstable(int n, const uint32_t* Kin, const int32_
         Kout[dst] = k;
         Vout[dst] = Vin[i];
     }
-    wave_lds_sync();
+    part_sync<G>();
     return m;
 }
 
 // Every low-digit bucket small (uniform rows): each key's place in its bucket by a direct rank on
 // (key, position) (positions are distinct, so the order is total and the sort stable).
+template <bool G>
 __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, uint32_t* K0, int32_t* V0,
                                   const uint32_t* start) {
     constexpr int dm = (1 << kWideDigit) - 1;
@@ -800,7 +819,7 @@ __device__ void wave_rank_buckets(int n, const uint32_t* K1, const int32_t* V1, 
         K0[bs + rank] = ki;
         V0[bs + rank] = vi;
     }
-    wave_lds_sync();
+    part_sync<G>();
 }
 
 // One lane's segment of a tile of the sorted part, as its flat record: kind 1 = a chunk (a =
@@ -895,9 +914,9 @@ struct SegPass {
 // on the low byte and a within-bucket rank on (key, position); narrow keys, or buckets too big to
 // rank (skewed rows), by stable LSD counting passes.  Then classifies the segments (LDS only), reserves the wave's ranges of the flat item lists and arrives in one packed atomic
 // add, stores the per-table outputs while it is in flight, then the flat records at its return.
+template <bool G>
 __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
-                               int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, WaveBuildLds& sl,
-                               int g, int groups) {
+                               int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, int g, int groups) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lanes_below();
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
@@ -906,17 +925,17 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
-    if (n > 1 && nbits > 8 && wave_count_pass_unstable(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
+    if (n > 1 && nbits > 8 && wave_count_pass_unstable<G>(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
         WPH(3);
-        wave_rank_buckets(n, K1, V1, K0, V0, cnt);
+        wave_rank_buckets<G>(n, K1, V1, K0, V0, cnt);
     } else if (n > 1 && nbits > 0) {  // narrow keys, or skewed rows: stable LSD passes from (K0, V0)
-        wave_count_pass(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
+        wave_count_pass<G>(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
         WPH(3);
         Ks = K1;
         Vs = V1;
         for (int shift = 8; shift < nbits; shift += 8) {
             const bool from1 = Ks == K1;
-            wave_count_pass(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
+            wave_count_pass<G>(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
                             from1 ? K0 : K1, from1 ? V0 : V1, R, cnt);
             Ks = from1 ? K0 : K1;
             Vs = from1 ? V0 : V1;
@@ -975,7 +994,7 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
         C += (tot >> 10) & 1023;
         H += tot >> 20;
     }
-    wave_lds_sync();
+    part_sync<G>();
     int S = 0;
     if (H)  // (rows hit more than kChunk times in this part: small tables)
         for (int s0 = 0; s0 < U; s0 += 64) {
@@ -1037,143 +1056,190 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     WPH(6);
 }
 
-// One build workgroup (kWaveParts waves = 256 threads): parts q0 .. q0 + 3 (q0 = 4 (g mod P / 4))
-// of table t = g / (P / 4), P = 2^vs >= 4 parts per table.  Every thread of the workgroup calls
-// it.  The four waves first split the table's positions among the four parts together -- wave w
-// reads positions [512 w, 512 w + 512), 16-B loads, and the parts' lists keep position order by
-// (wave, piece, lane) offsets from DPP scans and one exchange of per-wave counts -- then wave q
-// sorts part q0 + q alone (wave_sort_part).  The last of the T P / 4 workgroups to arrive
-// publishes the flat lists' totals (finish_item_lists).
-__device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
-                                 const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
-                                 unsigned* __restrict__ err, WaveBuildLds& sl) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
-    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+// One round of a build wave's index loads: positions 2048 r + 512 w + 256 k + 4 lane + e (k < 2,
+// e < 4) of table t, decoded: rv[j] = row >> vs, code (3 bits per element j = 4 k + e) = its part - q0
+// (0..3) or 4 (another workgroup's part, past N, or out of range), and per piece k and part q this
+// lane's exclusive prefix over the wave (pre) and the wave's total (ptot), by DPP scans of two 16-bit
+// fields per word.  bad: an out-of-range index among this lane's.
+struct WaveRound {
+    uint32_t rv[8];
+    uint32_t code;
+    bool bad;
+    int pre[2][kWaveParts], ptot[2][kWaveParts];
+};
+
+__device__ __forceinline__ void wave_round(WaveRound& o, int r, int w, int t, int q0, int vs, uint32_t nrows,
+                                           const void* __restrict__ idx, int itype, int64_t tstride, int base, int N) {
+    constexpr int PK = 2;
+    const int lane = threadIdx.x & 63;
     const uint32_t pmask = (1u << vs) - 1u;
-    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
-    constexpr int WS = kStepIndexMaxN / kWaveParts;  // positions per wave
-    constexpr int PK = WS / 256;                     // 16-B pieces per lane
-    WPH(0);
-    // element j = 4 k + e: position WS w + 256 k + 4 lane + e; code = its part - q0 (0..3), or 4
-    uint32_t rv[4 * PK];
-    uint32_t code = 0;  // 3 bits per element
-    bool bad = false;
-    {
-        const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
-        const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
-        const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
-        int64_t r[4 * PK];
-        bool in[4 * PK];
-        if (vec && itype == DLRM_I32) {
-            int4 q[PK];
+    const int p0 = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w;
+    const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+    const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
+    const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
+    int64_t rr[4 * PK];
+    bool in[4 * PK];
+    if (vec && itype == DLRM_I32) {
+        int4 q[PK];
 #pragma unroll
-            for (int k = 0; k < PK; ++k)
-                if (WS * w + 256 * k < N) q[k] = ldg<int4>(i32 + WS * w + 256 * k + 4 * lane);
+        for (int k = 0; k < PK; ++k)
+            if (p0 + 256 * k < N) q[k] = ldg<int4>(i32 + p0 + 256 * k + 4 * lane);
 #pragma unroll
-            for (int k = 0; k < PK; ++k) {
-                const bool kin = WS * w + 256 * k < N;
-                r[4 * k] = q[k].x; r[4 * k + 1] = q[k].y; r[4 * k + 2] = q[k].z; r[4 * k + 3] = q[k].w;
+        for (int k = 0; k < PK; ++k) {
+            const bool kin = p0 + 256 * k < N;
+            rr[4 * k] = q[k].x; rr[4 * k + 1] = q[k].y; rr[4 * k + 2] = q[k].z; rr[4 * k + 3] = q[k].w;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) in[4 * k + e] = kin;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4 * PK; ++j) {
-                const int pj = WS * w + 256 * (j >> 2) + 4 * lane + (j & 3);
-                in[j] = pj < N;
-                r[j] = load_index_if(in[j], idx, itype, (int64_t)t * tstride + pj);
-            }
+            for (int e = 0; e < 4; ++e) in[4 * k + e] = kin;
         }
-        WPH(7);
+    } else {
 #pragma unroll
         for (int j = 0; j < 4 * PK; ++j) {
-            const int64_t rr = r[j] - base;
-            const bool ok = in[j] && (uint64_t)rr < (uint64_t)nrows;  // (negative: a huge unsigned)
-            bad |= in[j] && !ok;
-            const uint32_t pq = ((uint32_t)rr & pmask) - (uint32_t)q0;
-            code |= (ok && pq < (uint32_t)kWaveParts ? pq : 4u) << (3 * j);
-            rv[j] = (uint32_t)rr >> vs;
+            const int pj = p0 + 256 * (j >> 2) + 4 * lane + (j & 3);
+            in[j] = pj < N;
+            rr[j] = load_index_if(in[j], idx, itype, (int64_t)t * tstride + pj);
         }
     }
-    // out of range raises BoundsError; the workgroup of parts 0..3 reports it
-    if (q0 == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
-    // per piece k and part q: this lane's count, a DPP scan over the lanes (two 16-bit fields per word)
-    int pre[PK][kWaveParts], ptot[PK][kWaveParts];
+    WPH(7);
+    o.code = 0;
+    o.bad = false;
+#pragma unroll
+    for (int j = 0; j < 4 * PK; ++j) {
+        const int64_t x = rr[j] - base;
+        const bool ok = in[j] && (uint64_t)x < (uint64_t)nrows;  // (negative: a huge unsigned)
+        o.bad |= in[j] && !ok;
+        const uint32_t pq = ((uint32_t)x & pmask) - (uint32_t)q0;
+        o.code |= (ok && pq < (uint32_t)kWaveParts ? pq : 4u) << (3 * j);
+        o.rv[j] = (uint32_t)x >> vs;
+    }
 #pragma unroll
     for (int k = 0; k < PK; ++k) {
         int cq[kWaveParts] = {0, 0, 0, 0};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const uint32_t cd = (code >> (3 * (4 * k + e))) & 7u;
+            const uint32_t cd = (o.code >> (3 * (4 * k + e))) & 7u;
 #pragma unroll
             for (int q = 0; q < kWaveParts; ++q) cq[q] += cd == (uint32_t)q ? 1 : 0;
         }
         const int a = cq[0] | (cq[1] << 16), b = cq[2] | (cq[3] << 16);
         const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
         const int ta = lane63(ia), tb = lane63(ib);
-        pre[k][0] = (ia - a) & 0xffff; pre[k][1] = (ia - a) >> 16;
-        pre[k][2] = (ib - b) & 0xffff; pre[k][3] = (ib - b) >> 16;
-        ptot[k][0] = ta & 0xffff; ptot[k][1] = ta >> 16; ptot[k][2] = tb & 0xffff; ptot[k][3] = tb >> 16;
+        o.pre[k][0] = (ia - a) & 0xffff; o.pre[k][1] = (ia - a) >> 16;
+        o.pre[k][2] = (ib - b) & 0xffff; o.pre[k][3] = (ib - b) >> 16;
+        o.ptot[k][0] = ta & 0xffff; o.ptot[k][1] = ta >> 16; o.ptot[k][2] = tb & 0xffff; o.ptot[k][3] = tb >> 16;
     }
-    if (lane < kWaveParts) {
-        int tw = 0;
+}
+
+// One build workgroup (kWaveParts waves = 256 threads): parts q0 .. q0 + 3 (q0 = 4 (g mod P / 4))
+// of table t = g / (P / 4), P = 2^vs >= 4 parts per table.  Every thread of the workgroup calls
+// it.  The four waves first split the table's positions among the four parts together -- in rounds
+// of 2048 positions, wave w reading positions [2048 r + 512 w, + 512), 16-B loads, and the parts'
+// lists keep position order by (round, wave, piece, lane) offsets from DPP scans and one exchange
+// of per-wave counts -- then wave q sorts part q0 + q alone (wave_sort_part).  Up to 2048
+// positions (one round) the loads are kept in registers across the exchange; beyond, a second pass
+// reloads them (from L2) to place them.  When the four parts overflow the LDS pool (their positions
+// total more than 2048: a tiny table's few rows, or hot rows, at large N) the parts are placed and
+// sorted in HBM scratch instead (ix.wscratch; the same sort, G = true).  The last of the T P / 4
+// workgroups to arrive publishes the flat lists' totals (finish_item_lists).
+// BIG = false: N <= 2048 (one round, the pool never overflows) -- the forward launch's build, whose
+// registers the HBM path would crowd; BIG = true: any N <= kWaveMaxN.
+template <bool BIG = true>
+__device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
+                                 const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
+                                 unsigned* __restrict__ err, WaveBuildLds& sl) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
+    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
+    const int R = BIG ? (N + kStepIndexMaxN - 1) / kStepIndexMaxN : 1;  // rounds (<= kWaveMaxN / 2048)
+    WPH(0);
+    WaveRound rd;
+    bool bad = false;
+    for (int r = 0; r < R; ++r) {  // pass 1: count
+        wave_round(rd, r, w, t, q0, vs, nrows, idx, itype, tstride, base, N);
+        bad |= rd.bad;
+        if (lane < kWaveParts) {
+            int tw = 0;
 #pragma unroll
-        for (int k = 0; k < PK; ++k)
+            for (int k = 0; k < 2; ++k)
 #pragma unroll
-            for (int q = 0; q < kWaveParts; ++q) tw += lane == q ? ptot[k][q] : 0;
-        sl.tot[w][lane] = tw;
-    }
-    __syncthreads();
-    // part q's region of the pool, and this wave's offset in it
-    int pbase[kWaveParts], woff[kWaveParts], n_of[kWaveParts];
-    {
-        int run = 0;
-#pragma unroll
-        for (int q = 0; q < kWaveParts; ++q) {
-            int nq = 0, wq = 0;
-#pragma unroll
-            for (int ww = 0; ww < kWaveParts; ++ww) {
-                const int c = sl.tot[ww][q];
-                nq += c;
-                wq += ww < w ? c : 0;
-            }
-            pbase[q] = run;
-            woff[q] = wq;
-            n_of[q] = nq;
-            run += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
+                for (int q = 0; q < kWaveParts; ++q) tw += lane == q ? rd.ptot[k][q] : 0;
+            sl.tot[r][w][lane] = tw;
         }
     }
+    // out of range raises BoundsError; the workgroup of parts 0..3 reports it
+    if (q0 == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    __syncthreads();
+    // part q's size, its region (pool: 16-B aligned, in part order; HBM: its own virtual table's),
+    // and the offset of each round's share of wave w in it
+    int n_of[kWaveParts], pbase[kWaveParts], total = 0;
+#pragma unroll
+    for (int q = 0; q < kWaveParts; ++q) {
+        int nq = 0;
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int ww = 0; ww < kWaveParts; ++ww) nq += sl.tot[r][ww][q];
+        n_of[q] = nq;
+        pbase[q] = total;
+        total += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
+    }
+    const bool G = BIG && total > kStepIndexMaxN;  // (uniform over the workgroup)
     WPH(1);
-#pragma unroll
-    for (int k = 0; k < PK; ++k) {
-        int at[kWaveParts];
+    for (int r = R - 1; r >= 0; --r) {  // pass 2: place (round R - 1 is still in registers)
+        if (r != R - 1) wave_round(rd, r, w, t, q0, vs, nrows, idx, itype, tstride, base, N);
+        int at0[kWaveParts];
 #pragma unroll
         for (int q = 0; q < kWaveParts; ++q) {
-            int before = 0;
+            int before = 0;  // earlier rounds, then this round's earlier waves
+            for (int rr = 0; rr < r; ++rr)
 #pragma unroll
-            for (int kk = 0; kk < k; ++kk) before += ptot[kk][q];
-            at[q] = pbase[q] + woff[q] + before + pre[k][q];
+                for (int ww = 0; ww < kWaveParts; ++ww) before += sl.tot[rr][ww][q];
+#pragma unroll
+            for (int ww = 0; ww < kWaveParts; ++ww) before += ww < w ? sl.tot[r][ww][q] : 0;
+            at0[q] = (G ? 0 : pbase[q]) + before;
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint32_t cd = (code >> (3 * (4 * k + e))) & 7u;
-            if (cd < (uint32_t)kWaveParts) {
-                int dst = 0;
+        for (int k = 0; k < 2; ++k) {
+            int at[kWaveParts];
 #pragma unroll
-                for (int q = 0; q < kWaveParts; ++q)
-                    if (cd == (uint32_t)q) dst = at[q]++;
-                sl.K[0][dst] = rv[4 * k + e];
-                sl.V[0][dst] = WS * w + 256 * k + 4 * lane + e;
+            for (int q = 0; q < kWaveParts; ++q) at[q] = at0[q] + (k ? rd.ptot[0][q] : 0) + rd.pre[k][q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t cd = (rd.code >> (3 * (4 * k + e))) & 7u;
+                if (cd < (uint32_t)kWaveParts) {
+                    int dst = 0;
+#pragma unroll
+                    for (int q = 0; q < kWaveParts; ++q)
+                        if (cd == (uint32_t)q) dst = at[q]++;
+                    const int32_t pos = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w + 256 * k + 4 * lane + e;
+                    if (G) {
+                        const int64_t vo = (int64_t)((t << vs) + q0 + (int)cd) * ix.cap + dst;
+                        ix.wscratch[vo] = rd.rv[4 * k + e];
+                        ((int32_t*)ix.wscratch)[ix.wstride + vo] = pos;
+                    } else {
+                        sl.K[0][dst] = rd.rv[4 * k + e];
+                        sl.V[0][dst] = pos;
+                    }
+                }
             }
         }
     }
+    if (G) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
+    if (G) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // wave w sorts part q0 + w
-    const int pb = pbase[w], n = n_of[w];
+    const int n = n_of[w];
     const int v = (t << vs) + q0 + w;
-    wave_sort_part(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
-                   sl.cnt[w], sl, g, (T << vs) / kWaveParts);
+    const int groups = (T << vs) / kWaveParts;
+    if (BIG && G) {
+        uint32_t* K0 = ix.wscratch + (int64_t)v * ix.cap;
+        const int64_t S = ix.wstride;
+        wave_sort_part<true>(ix, v, t, vs, nrows, n, K0, (int32_t*)(K0 + S), K0 + 2 * S, (int32_t*)(K0 + 3 * S),
+                             (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
+    } else {
+        const int pb = pbase[w];
+        wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb,
+                              sl.R + pb, sl.cnt[w], g, groups);
+    }
 }
 
 }  // namespace dlrm

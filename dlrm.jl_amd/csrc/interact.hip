@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256, 3) void interact_fwd_index_kernel(int d, int F
 #endif
     if ((int)blockIdx.x < NI) {
         if (wave) {
-            wave_build_group(ix, blockIdx.x, T_, ga.tabs, ga.idx, ga.itype, ga.tstride, ga.base, B * ga.L, ga.err,
+            wave_build_group<false>(ix, blockIdx.x, T_, ga.tabs, ga.idx, ga.itype, ga.tstride, ga.base, B * ga.L, ga.err,
                              *(WaveBuildLds*)smem);
         } else {
             StepLds& sl = *(StepLds*)smem;

@@ -355,7 +355,8 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 // positions.  Workgroup b takes items b, b + grid, ...: every item is short, so static striding
 // balances, and no workgroup is launched past the work.
 // MODE 0: chunks + hot slices; 1: + once-hit (singles) items; 2: + the next batch's split indexer
-// in the first pa.T << pa.ix.vshift workgroups (PrepArgs).
+// in the first (pa.T << pa.ix.vshift) / 4 workgroups (PrepArgs); 3: the same for more than 2048
+// positions per table.
 #ifndef DLRM_BUILD_PRIO
 #define DLRM_BUILD_PRIO 3
 #endif
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
                                                                   PrepArgs pa) {
     constexpr bool SG = MODE == 1;
     int bid = blockIdx.x, nblk = gridDim.x;
-    if (MODE == 2) {
+    if (MODE >= 2) {
         extern __shared__ __attribute__((aligned(16))) unsigned char prep_lds[];
         const int NI = (pa.T << pa.ix.vshift) / kWaveParts;
         if (bid < NI) {  // the next batch's split build: one wave per table part (indexer.hpp)
@@ -378,8 +379,10 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
             // 54.72 / 54.77 -> 54.91 / 55.04 M samples/s, apply 10.58 -> 10.45 us)
             __builtin_amdgcn_s_setprio(kBuildPrio);
             ITEM_START(4, 0, bid);
-            wave_build_group(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
-                             *(WaveBuildLds*)prep_lds);
+            // (MODE 3: the build of more than 2048 positions per table -- rounds and the HBM overflow
+            // path -- in its own instantiation, so the step's MODE 2 kernel keeps its registers)
+            wave_build_group<MODE == 3>(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N,
+                                        pa.err, *(WaveBuildLds*)prep_lds);
             ITEM_END(0);
             return;
         }
@@ -530,8 +533,12 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
 // The step indexer's workgroups alone (PrepArgs), where the apply has no vector kernel to host them.
 __global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    wave_build_group(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
-                     *(WaveBuildLds*)lds);
+    if (pa.N <= kStepIndexMaxN)
+        wave_build_group<false>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
+                                *(WaveBuildLds*)lds);
+    else
+        wave_build_group<true>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
+                               *(WaveBuildLds*)lds);
 }
 
 // step_index_kernel's own launch (the next batch's split build when the apply launch cannot carry it)
@@ -724,14 +731,23 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     // (the once-hit items and the next batch's indexer are separate instantiations: the step's
     // apply stays lean)
     if (pa && !sa.single) {
-        static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           (int)sizeof(WaveBuildLds));
-        (void)attr;
+        static const hipError_t attr2 = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                            (int)sizeof(WaveBuildLds));
+        static const hipError_t attr3 = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 3>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                            (int)sizeof(WaveBuildLds));
+        (void)attr2;
+        (void)attr3;
         const int NI = (pa->T << pa->ix.vshift) / kWaveParts;
-        hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
-                           sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa,
-                           *pa);
+        if (pa->N <= kStepIndexMaxN)
+            hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
+                               sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
+                               sa, *pa);
+        else
+            hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 3>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
+                               sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
+                               sa, *pa);
     } else if (sa.single) {
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 1>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
                            tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});

@@ -126,6 +126,7 @@ class HipShardOps:
         self.Bg, self.L, self.lr, self.base = batch_global, lookups, lr, index_base
         self.indexer = SparseIndexer(len(tables), batch_global * lookups, self.device) if tables else None
         self.rts = self.ident = None
+        self._prepare = None  # None: not tried yet; False: the wave build does not take this shape
 
     def _ok(self, rc):
         if rc != _lib.OK:
@@ -140,6 +141,18 @@ class HipShardOps:
         self.ident = PackedIndices(ar.repeat(T, 1).reshape(T, Bm, 1))
 
     def build_indexer(self, idx):
+        """The update's split indexer over the global batch: the wave build (dlrm_indexer_prepare,
+        one-hot, <= 16384 positions per table: 16 parts per 2048 positions, one wave each) where it
+        applies, else dlrm_indexer_build (in-LDS or hash build)."""
+        if idx.L == 1 and self._prepare is not False:
+            rc = self.lib.dlrm_indexer_prepare(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
+                                               idx.itype, idx.stride, self.base, idx.B)
+            if rc == _lib.OK:
+                self._prepare = True
+                return
+            if rc != _lib.E_UNSUPPORTED:
+                self.ctx.check(rc)
+            self._prepare = False
         self._ok(self.lib.dlrm_indexer_build(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
                                              idx.itype, idx.stride, self.base, idx.B, idx.L))
 

@@ -111,6 +111,24 @@ class SparseIndexer:
         self._built_from = idx
         return self
 
+    def prepare(self, tables, indices, *, index_base=1):
+        """The training step's split build of `indices` (one-hot, <= 16384 positions per table, <= 31
+        tables) as its own launch (dlrm_indexer_prepare: the wave build): a following dlrm_step_fwd of
+        these indices only gathers, and update_ / dlrm_sgd_update(PREBUILT) take its once-hit
+        positions as well.  Returns False where the wave build does not apply (use build())."""
+        ts = as_table_set(tables)
+        idx = PackedIndices(indices, device=ts.device)
+        require_device(idx.data, ts.device, "indices")
+        if idx.L != 1 or idx.B > self.capacity or idx.T != self.num_tables:
+            return False
+        rc = self.ctx.lib.dlrm_indexer_prepare(self.ctx.bind(), self.handle, ts.handle, ptr(idx.data), idx.itype,
+                                               idx.stride, index_base, idx.B)
+        if rc == _lib.E_UNSUPPORTED:
+            return False
+        self.ctx.check(rc)
+        self._built_from = idx
+        return True
+
     def state(self):
         """Host-side state of the last build: a mask of _lib.IX_* bits (no GPU call)."""
         st = ctypes.c_uint()

@@ -267,6 +267,68 @@ def test_step_fwd_indexer_parts(pkg, gpu, rows, B, zipf):
     _assert_segments(hp.indexer, idx, B)
 
 
+@pytest.mark.parametrize("rows,B,zipf,case", [
+    ("kaggle", 2048, None, ""), ("kaggle", 8192, None, ""),          # tiny tables overflow the pool at 8192
+    ([3, 4, 10, 1000, 5_000_000], 16384, None, ""), ([300, 100000, 3, 5_000_000], 6000, 1.1, ""),
+    ([500, 2000, 1_000_000], 16384, 1.5, ""),                          # hot rows: multi-row parts in HBM
+    ([1], 16384, None, ""), ([0x10000, 0x1000000], 3000, None, ""), ([7, 70000], 2049, None, ""),
+    ([1000], 16384, None, "one-part"),                                 # every index in one part: 8 rows
+    ([5000, 3], 4100, 1.05, "")])
+def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
+    """dlrm_indexer_prepare (the wave build: 16 parts per 2048 positions, rounds of 2048 positions,
+    parts that overflow a workgroup's LDS pool sorted in HBM) up to 16384 positions per table: unique
+    rows and per-row positions exactly numpy's, every once-hit flag right."""
+    if rows == "kaggle":
+        rows = pkg.KAGGLE_EMBEDDING_SIZES
+    rng = np.random.default_rng(B + len(rows) + 3)
+    idx = rand_indices(rng, rows, B, 1, zipf=zipf)
+    if case == "one-part":  # rows 5 + 128 k: all in part 5 of 128
+        idx = (5 + 128 * rng.integers(0, 7, size=(1, B))).astype(idx.dtype)
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B, gpu)
+    assert ix.prepare(tabs, torch.from_numpy(idx).to(torch.int32).to(gpu), index_base=0)
+    tabs.ctx.check_bounds()
+    _assert_segments(ix, idx, B)
+
+
+def test_prepared_step_equals_fresh_step_and_bounds(pkg, gpu):
+    """dlrm_indexer_prepare -> dlrm_step_fwd (gather only: the indexer is prepared) ->
+    dlrm_step_bwd equals a step whose forward builds its own indexer, bit for bit; an out-of-range
+    index in the prepared batch raises BoundsError and leaves every table unchanged."""
+    rows, D, B = [3, 40, 100000, 7, 2_000_000], 64, 2048
+    rng = np.random.default_rng(61)
+    tabs = rand_tables(rng, rows, D)
+    idx_np = rand_indices(rng, rows, B, 1)
+    p = pkg.PackedIndices(torch.from_numpy(idx_np).to(torch.int32).to(gpu))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = len(rows) + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0)
+    assert hp.indexer.prepare(hp.ts, p, index_base=0)
+    assert hp.indexer.state() & pkg._lib.IX_PREPARED
+    hp.step_fwd(x, p)
+    hp.step_bwd(dout, x=x, idx=p)
+    torch.cuda.synchronize()
+    hp.check_bounds()
+    ref = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0)
+    ref.step(x, p, dout)
+    torch.cuda.synchronize()
+    assert torch.equal(hp.out, ref.out) and torch.equal(hp.dx, ref.dx)
+    for a, b in zip(hp.ts, ref.ts):
+        assert torch.equal(a.data, b.data)
+    bad_np = idx_np.copy()
+    bad_np[2, 77] = rows[2] + 9
+    bad = pkg.PackedIndices(torch.from_numpy(bad_np).to(torch.int32).to(gpu))
+    hp2 = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0)
+    assert hp2.indexer.prepare(hp2.ts, bad, index_base=0)
+    hp2.step_fwd(x, bad)
+    hp2.step_bwd(dout, x=x, idx=bad)
+    with pytest.raises(pkg.BoundsError):
+        hp2.check_bounds()
+    for t in range(len(rows)):
+        assert np.array_equal(to_np_f32(hp2.ts[t].data), tabs[t]), f"table {t} was written on a BoundsError step"
+
+
 def _assert_segments(ix, idx, N):
     """One segment per distinct row (segment order unspecified), holding exactly that row's
     positions in ascending order (vectorised: large-N builds have ~N segments per table)."""
@@ -1146,6 +1208,9 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
 @pytest.mark.parametrize("rows,D,B,dtype", [("kaggle", 128, 2048, torch.float32),
                                             ("kaggle", 16, 2048, torch.float32),
                                             ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32),
+                                            # configs[2]'s shape: the in-apply wave build at 8192
+                                            ("kaggle", 128, 8192, torch.bfloat16),
+                                            ([3, 500, 100000, 2_000_000], 32, 16384, torch.float32),
                                             ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16),
                                             # Terabyte-shaped bf16 x 128 at B = 2048: the in-apply
                                             # build runs 8 parts per table (256-B rows)
