@@ -53,7 +53,12 @@ struct dlrm_indexer {
     bool split = false;  // built by dlrm_step_fwd's kernel: once-hit rows are left to the backward
     bool prepared = false;  // built by dlrm_step_bwd_prepare for the next dlrm_step_fwd (not yet consumed)
     bool singles_done = false;  // a split backward has applied this build's once-hit rows already
-    unsigned* prep_err = nullptr;  // device word: bounds errors of a prepared build (the forward re-raises)
+    // device word for the bounds errors of the NEXT batch's build inside an apply launch
+    // (dlrm_step_bwd_prepare): it must not be the ctx's flag, which that launch's apply items read to
+    // decide whether to write (a race); nothing reads it -- the next forward gathers the same
+    // indices and raises their errors on the ctx's flag.  (dlrm_indexer_prepare, its own launch,
+    // raises on the ctx's flag directly.)
+    unsigned* prep_err = nullptr;
     const void* indices = nullptr;
     int itype = 0, base = 0, B = 0, L = 0;
     int64_t tstride = 0;

@@ -116,6 +116,23 @@ __device__ __forceinline__ void store4(T* p, const f32x4_t& v) {
     }
 }
 
+// Elements [lo, hi) of a staged output row (LDS) to orow, 16-B stores between a head (up to the
+// row's first 16-B boundary at or after lo) and a tail; lt = this lane's index among the NL lanes.
+template <typename T, int NL>
+__device__ __forceinline__ void store_staged(T* orow, const float* stage, int lo, int hi, int lt) {
+    const int e0 = lo + (int)((4 - (((uintptr_t)(orow + lo) >> 2) & 3)) & 3);
+    const int hend = e0 < hi ? e0 : hi;
+    if (lo + lt < hend) stg<T>(orow + lo + lt, from_f32<T>(stage[lo + lt]));
+    if (e0 >= hi) return;
+    const int nv = (hi - e0) >> 2;
+    for (int k = lt; k < nv; k += NL) {
+        const int e = e0 + 4 * k;
+        stg<f32x4_t>((f32x4_t*)(orow + e), f32x4_t{stage[e], stage[e + 1], stage[e + 2], stage[e + 3]});
+    }
+    const int et = e0 + 4 * nv + lt;
+    if (lt < 4 && et < hi) stg<T>(orow + et, from_f32<T>(stage[et]));
+}
+
 template <typename T, int NB> struct FwdPart {
     static constexpr int NT = NB * (NB + 1) / 2;  // lower-triangle tiles
 };
@@ -152,6 +169,19 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
     // the staged output row leaves as 16-B stores when every row start is aligned for them (fp32 at
     // d = 128: forward 12.1 -> 11.4 us, r8d; at d = 16 and for bf16 rows no gain: scalar stores)
     constexpr bool VEC_OUT = kFwdVecOut && sizeof(T) == 4 && DC >= 128;
+    // fp32 rows whose start is not 16-B aligned (W % 4 != 0): 16-B stores between a head and a tail
+#ifndef DLRM_FWD_VEC_ROW
+#define DLRM_FWD_VEC_ROW 1
+#endif
+    constexpr bool VEC_ROW = DLRM_FWD_VEC_ROW && sizeof(T) == 4 && DC >= 128;
+    // EARLY: the first Gram tile (pairs i < 16) and x go out while the MFMAs of the other two tiles
+    // run: tile-outer MFMA order (each tile's summation order unchanged: bit-identical output)
+#ifndef DLRM_FWD_EARLY
+#define DLRM_FWD_EARLY 0
+#endif
+    constexpr bool EARLY = DLRM_FWD_EARLY && VEC_ROW && WPS == 1 && !CONTIG && NB == 2 && DC > 0 && DC == CBLK;
+    const int F16 = F < 16 ? F : 16;
+    const int E1 = d + F16 * (F16 - 1) / 2;  // EARLY: x + the pairs of tile 00
     const bool vec_out = W % 4 == 0 && out_ld % 4 == 0 && ((uintptr_t)out & (4 * sizeof(T) - 1)) == 0;
     bool bad_any = false;  // an out-of-range index was skipped (zero row) by this lane
     for (int64_t b0 = (int64_t)bid * SPB; b0 < B; b0 += (int64_t)nblocks * SPB) {
@@ -232,7 +262,39 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
 #pragma unroll
                 for (int I = 0; I < NB; ++I)
 #pragma unroll
-                    for (int J = 0; J <= I; ++J, ++ij) FR::mma(acc[NPART == 2 ? (CONTIG ? (((u0 + uu * FR::COLS) >> 6) & 1) : (uu & 1)) : 0][ij], a[v][I], a[v][J]);
+                    for (int J = 0; J <= I; ++J, ++ij)
+                        if (!EARLY || ij == 0)
+                            FR::mma(acc[NPART == 2 ? (CONTIG ? (((u0 + uu * FR::COLS) >> 6) & 1) : (uu & 1)) : 0][ij],
+                                    a[v][I], a[v][J]);
+            }
+            if constexpr (EARLY) {
+                // x (fast_vcat) and tile 00's pairs staged and stored now; tiles 10 and 11 after
+#pragma unroll
+                for (int v = 0; v < UV; ++v) {
+                    const int col = u0 + v * FR::COLS + q * FR::PER_LANE;
+                    if (c == 0 && col < d) {
+                        float f[FR::PER_LANE];
+                        FR::to_f(f, a[v][0]);
+#pragma unroll
+                        for (int k = 0; k < FR::PER_LANE; k += 4)
+                            *(f32x4_t*)(stage + col + k) = f32x4_t{f[k], f[k + 1], f[k + 2], f[k + 3]};
+                    }
+                }
+                const f32x4_t z0 = acc[0][0] + acc[NPART - 1][0];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 4 * q + r;
+                    if (i < F && c < i) stage[d + i * (i - 1) / 2 + c] = z0[r];
+                }
+                wave_lds_sync();
+                if (live) store_staged<T, 64>(orow, stage, 0, E1, lane);
+#pragma unroll
+                for (int v = 0; v < UV; ++v) {
+                    const int uu = v;
+                    if (!(uu * FR::COLS < DC)) continue;
+                    FR::mma(acc[NPART == 2 ? (uu & 1) : 0][1], a[v][1], a[v][0]);
+                    FR::mma(acc[NPART == 2 ? (uu & 1) : 0][2], a[v][1], a[v][1]);
+                }
             }
             // fast_vcat: x (row 0: lanes c == 0 of I = 0) into the output head, and the lookup
             // output ys rows (FUSED with ys kept), from the fragments (after the MFMAs, so the MFMAs
@@ -242,7 +304,7 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
                 const int uu = CONTIG ? h * UV + v : WPS * v + h;
                 const int col = u0 + uu * FR::COLS + q * FR::PER_LANE;
                 if (col < d && live) {
-                    if (c == 0) {
+                    if (c == 0 && !EARLY) {
                         float f[FR::PER_LANE];
                         FR::to_f(f, a[v][0]);
                         if (staged) {
@@ -253,8 +315,8 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
 #pragma unroll
                             for (int k = 0; k < FR::PER_LANE; ++k) stg<T>(orow + col + k, from_f32<T>(f[k]));
                         }
-                        if (yb) stg<frag>(yb + col, a[v][0]);
                     }
+                    if (c == 0 && yb) stg<frag>(yb + col, a[v][0]);
                     if (FUSED && yb) {
 #pragma unroll
                         for (int I = 0; I < NB; ++I) {
@@ -289,6 +351,7 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
             for (int I = 0; I < NB; ++I)
 #pragma unroll
                 for (int J = 0; J <= I; ++J, ++ij) {
+                    if (EARLY && ij == 0) continue;  // (staged and stored already)
                     const int j = J * 16 + c;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -307,10 +370,16 @@ __device__ __forceinline__ void fwd_body_onehot(int bid, int nblocks, float* sta
         }
         if (staged) {
             if constexpr (WPS == 1) wave_lds_sync(); else __syncthreads();
-            if (live && VEC_OUT && vec_out)
+            if (live && VEC_OUT && vec_out) {
                 for (int e = 4 * (lane + 64 * h); e < W; e += 256 * WPS) store4<T>(orow + e, *(const f32x4_t*)(stage + e));
-            else if (live)
+            } else if (live && VEC_ROW) {
+                // rows of W = d + P floats start at any 4-B boundary (479 at the metric config): the
+                // head elements up to the row's first 16-B boundary, then 16-B stores of the staged
+                // row (read from LDS as four floats), then the tail (EARLY: [E1, W) only)
+                store_staged<T, 64 * WPS>(orow, stage, EARLY ? E1 : 0, W, lane + 64 * h);
+            } else if (live) {
                 for (int e = lane + 64 * h; e < W; e += 64 * WPS) stg<T>(orow + e, from_f32<T>(stage[e]));
+            }
             if constexpr (WPS == 1) wave_lds_sync(); else __syncthreads();
         } else if constexpr (WPS == 2) {
             __syncthreads();  // xch is rewritten by the next pass

@@ -914,7 +914,10 @@ struct SegPass {
 // on the low byte and a within-bucket rank on (key, position); narrow keys, or buckets too big to
 // rank (skewed rows), by stable LSD counting passes.  Then classifies the segments (LDS only), reserves the wave's ranges of the flat item lists and arrives in one packed atomic
 // add, stores the per-table outputs while it is in flight, then the flat records at its return.
-template <bool G>
+// DIRECT: a part of one row (its table has <= 2^vs rows): the caller already wrote perm (positions in
+// order) and the once-hit flags; K0 / V0 hold the part's first (up to 8) keys / positions and R room
+// for one segment start -- the part is one segment, nothing is sorted.
+template <bool G, bool DIRECT = false>
 __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
                                int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, int g, int groups) {
     const int lane = threadIdx.x & 63;
@@ -925,7 +928,8 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
-    if (n > 1 && nbits > 8 && wave_count_pass_unstable<G>(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
+    if (DIRECT) {
+    } else if (n > 1 && nbits > 8 && wave_count_pass_unstable<G>(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
         WPH(3);
         wave_rank_buckets<G>(n, K1, V1, K0, V0, cnt);
     } else if (n > 1 && nbits > 0) {  // narrow keys, or skewed rows: stable LSD passes from (K0, V0)
@@ -953,7 +957,13 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
     const bool pvec = (ix.cap & 3) == 0;  // perm + i 16-B aligned
     int U = 0, C = 0, H = 0;
-    for (int j0 = 0; j0 < n; j0 += 256) {
+    if (DIRECT) {
+        U = n > 0 ? 1 : 0;
+        C = n >= 2 && n <= kChunk ? 1 : 0;
+        H = n > kChunk ? 1 : 0;
+        if (lane == 0) R[0] = 0;
+    }
+    for (int j0 = 0; j0 < (DIRECT ? 0 : n); j0 += 256) {
         const int i = j0 + 4 * lane;
         const uint4 k4 = *(const uint4*)(Ks + i);  // (past n: garbage, masked below)
         const int4 v4 = *(const int4*)(Vs + i);
@@ -1057,10 +1067,17 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
 }
 
 // One round of a build wave's index loads: positions 2048 r + 512 w + 256 k + 4 lane + e (k < 2,
-// e < 4) of table t, decoded: rv[j] = row >> vs, code (3 bits per element j = 4 k + e) = its part - q0
-// (0..3) or 4 (another workgroup's part, past N, or out of range), and per piece k and part q this
-// lane's exclusive prefix over the wave (pre) and the wave's total (ptot), by DPP scans of two 16-bit
-// fields per word.  bad: an out-of-range index among this lane's.
+// e < 4) of table t.  wave_round_load issues them (a caller loads the next round before decoding this
+// one, so one round's latency hides behind the other's work); wave_round_decode gives rv[j] =
+// row >> vs, code (3 bits per element j = 4 k + e) = its part - q0 (0..3) or 4 (another workgroup's
+// part, past N, or out of range), and per piece k and part q this lane's exclusive prefix over the
+// wave (pre) and the wave's total (ptot), by DPP scans of two 16-bit fields per word.  bad: an
+// out-of-range index among this lane's.
+struct WaveRaw {
+    int64_t rr[8];
+    bool in[8];
+};
+
 struct WaveRound {
     uint32_t rv[8];
     uint32_t code;
@@ -1068,17 +1085,15 @@ struct WaveRound {
     int pre[2][kWaveParts], ptot[2][kWaveParts];
 };
 
-__device__ __forceinline__ void wave_round(WaveRound& o, int r, int w, int t, int q0, int vs, uint32_t nrows,
-                                           const void* __restrict__ idx, int itype, int64_t tstride, int base, int N) {
+__device__ __forceinline__ WaveRaw wave_round_load(int r, int w, int t, const void* __restrict__ idx, int itype,
+                                                   int64_t tstride, int N) {
     constexpr int PK = 2;
     const int lane = threadIdx.x & 63;
-    const uint32_t pmask = (1u << vs) - 1u;
     const int p0 = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w;
     const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
     const int64_t* i64 = (const int64_t*)idx + (int64_t)t * tstride;
     const bool vec = N % 256 == 0 && (itype == DLRM_I32 ? (uintptr_t)i32 % 16 == 0 : (uintptr_t)i64 % 16 == 0);
-    int64_t rr[4 * PK];
-    bool in[4 * PK];
+    WaveRaw o;
     if (vec && itype == DLRM_I32) {
         int4 q[PK];
 #pragma unroll
@@ -1087,26 +1102,33 @@ __device__ __forceinline__ void wave_round(WaveRound& o, int r, int w, int t, in
 #pragma unroll
         for (int k = 0; k < PK; ++k) {
             const bool kin = p0 + 256 * k < N;
-            rr[4 * k] = q[k].x; rr[4 * k + 1] = q[k].y; rr[4 * k + 2] = q[k].z; rr[4 * k + 3] = q[k].w;
+            o.rr[4 * k] = q[k].x; o.rr[4 * k + 1] = q[k].y; o.rr[4 * k + 2] = q[k].z; o.rr[4 * k + 3] = q[k].w;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) in[4 * k + e] = kin;
+            for (int e = 0; e < 4; ++e) o.in[4 * k + e] = kin;
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 4 * PK; ++j) {
             const int pj = p0 + 256 * (j >> 2) + 4 * lane + (j & 3);
-            in[j] = pj < N;
-            rr[j] = load_index_if(in[j], idx, itype, (int64_t)t * tstride + pj);
+            o.in[j] = pj < N;
+            o.rr[j] = load_index_if(o.in[j], idx, itype, (int64_t)t * tstride + pj);
         }
     }
+    return o;
+}
+
+__device__ __forceinline__ void wave_round_decode(WaveRound& o, const WaveRaw& raw, int q0, int vs, uint32_t nrows,
+                                                  int base) {
+    constexpr int PK = 2;
+    const uint32_t pmask = (1u << vs) - 1u;
     WPH(7);
     o.code = 0;
     o.bad = false;
 #pragma unroll
     for (int j = 0; j < 4 * PK; ++j) {
-        const int64_t x = rr[j] - base;
-        const bool ok = in[j] && (uint64_t)x < (uint64_t)nrows;  // (negative: a huge unsigned)
-        o.bad |= in[j] && !ok;
+        const int64_t x = raw.rr[j] - base;
+        const bool ok = raw.in[j] && (uint64_t)x < (uint64_t)nrows;  // (negative: a huge unsigned)
+        o.bad |= raw.in[j] && !ok;
         const uint32_t pq = ((uint32_t)x & pmask) - (uint32_t)q0;
         o.code |= (ok && pq < (uint32_t)kWaveParts ? pq : 4u) << (3 * j);
         o.rv[j] = (uint32_t)x >> vs;
@@ -1154,8 +1176,12 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     WPH(0);
     WaveRound rd;
     bool bad = false;
-    for (int r = 0; r < R; ++r) {  // pass 1: count
-        wave_round(rd, r, w, t, q0, vs, nrows, idx, itype, tstride, base, N);
+    WaveRaw cur = wave_round_load(0, w, t, idx, itype, tstride, N);
+    for (int r = 0; r < R; ++r) {  // pass 1: count (the next round's loads in flight meanwhile)
+        WaveRaw nxt;
+        if (BIG && r + 1 < R) nxt = wave_round_load(r + 1, w, t, idx, itype, tstride, N);
+        wave_round_decode(rd, cur, q0, vs, nrows, base);
+        if (BIG) cur = nxt;
         bad |= rd.bad;
         if (lane < kWaveParts) {
             int tw = 0;
@@ -1182,10 +1208,19 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
         pbase[q] = total;
         total += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
     }
-    const bool G = BIG && total > kStepIndexMaxN;  // (uniform over the workgroup)
+    // a table of <= 2^vs rows: every part is one row (DIRECT: positions go straight to perm in order,
+    // nothing is sorted); else a workgroup whose parts overflow the pool sorts them in HBM (G)
+    const bool direct = BIG && nrows > 0 && ((nrows - 1) >> vs) == 0;
+    const bool G = BIG && !direct && total > kStepIndexMaxN;  // (uniform over the workgroup)
     WPH(1);
+    if (BIG && R > 1) cur = wave_round_load(R - 2, w, t, idx, itype, tstride, N);
     for (int r = R - 1; r >= 0; --r) {  // pass 2: place (round R - 1 is still in registers)
-        if (r != R - 1) wave_round(rd, r, w, t, q0, vs, nrows, idx, itype, tstride, base, N);
+        if (r != R - 1) {
+            WaveRaw nxt;
+            if (r > 0) nxt = wave_round_load(r - 1, w, t, idx, itype, tstride, N);
+            wave_round_decode(rd, cur, q0, vs, nrows, base);
+            cur = nxt;
+        }
         int at0[kWaveParts];
 #pragma unroll
         for (int q = 0; q < kWaveParts; ++q) {
@@ -1195,7 +1230,7 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
                 for (int ww = 0; ww < kWaveParts; ++ww) before += sl.tot[rr][ww][q];
 #pragma unroll
             for (int ww = 0; ww < kWaveParts; ++ww) before += ww < w ? sl.tot[r][ww][q] : 0;
-            at0[q] = (G ? 0 : pbase[q]) + before;
+            at0[q] = (G || direct ? 0 : pbase[q]) + before;
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -1211,7 +1246,17 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
                     for (int q = 0; q < kWaveParts; ++q)
                         if (cd == (uint32_t)q) dst = at[q]++;
                     const int32_t pos = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w + 256 * k + 4 * lane + e;
-                    if (G) {
+                    if (direct) {  // the part's perm entry and the position's once-hit flag, now
+                        int nq = 0;
+#pragma unroll
+                        for (int q = 0; q < kWaveParts; ++q) nq = cd == (uint32_t)q ? n_of[q] : nq;
+                        ix.perm[(int64_t)((t << vs) + q0 + (int)cd) * ix.cap + dst] = pos;
+                        ix.single[(int64_t)t * ix.cap + pos] = nq == 1 ? 1 : 0;
+                        if (dst < 8) {  // (the part's first positions: its chunk record carries 5 inline)
+                            sl.K[0][8 * (int)cd + dst] = rd.rv[4 * k + e];
+                            sl.V[0][8 * (int)cd + dst] = pos;
+                        }
+                    } else if (G) {
                         const int64_t vo = (int64_t)((t << vs) + q0 + (int)cd) * ix.cap + dst;
                         ix.wscratch[vo] = rd.rv[4 * k + e];
                         ((int32_t*)ix.wscratch)[ix.wstride + vo] = pos;
@@ -1230,7 +1275,10 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     const int n = n_of[w];
     const int v = (t << vs) + q0 + w;
     const int groups = (T << vs) / kWaveParts;
-    if (BIG && G) {
+    if (BIG && direct) {
+        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, sl.K[0] + 8 * w, sl.V[0] + 8 * w, sl.K[1] + 8 * w,
+                                    sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
+    } else if (BIG && G) {
         uint32_t* K0 = ix.wscratch + (int64_t)v * ix.cap;
         const int64_t S = ix.wstride;
         wave_sort_part<true>(ix, v, t, vs, nrows, n, K0, (int32_t*)(K0 + S), K0 + 2 * S, (int32_t*)(K0 + 3 * S),
