@@ -1176,12 +1176,35 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     WPH(0);
     WaveRound rd;
     bool bad = false;
-    WaveRaw cur = wave_round_load(0, w, t, idx, itype, tstride, N);
-    for (int r = 0; r < R; ++r) {  // pass 1: count (the next round's loads in flight meanwhile)
-        WaveRaw nxt;
-        if (BIG && r + 1 < R) nxt = wave_round_load(r + 1, w, t, idx, itype, tstride, N);
-        wave_round_decode(rd, cur, q0, vs, nrows, base);
-        if (BIG) cur = nxt;
+    // BIG with 16-B int32 index loads: rounds in batches of RB, each batch's loads issued together
+    // (one latency per batch, not per round); otherwise round by round
+    constexpr int RB = BIG ? 2 : 1;
+    const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+    const bool vec32 = BIG && itype == DLRM_I32 && N % 256 == 0 && (uintptr_t)i32 % 16 == 0;
+    int4 qa[RB][2];
+    auto load_batch = [&](int r0) {  // (vec32) rounds r0 .. r0 + RB - 1
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int p = kStepIndexMaxN * (r0 + j) + (kStepIndexMaxN / kWaveParts) * w + 256 * k;
+                if (r0 + j < R && p < N) qa[j][k] = ldg<int4>(i32 + p + 4 * lane);
+            }
+    };
+    auto raw_of = [&](int r, int j) {  // (vec32) round r = r0 + j's raw indices from registers
+        WaveRaw o;
+        const int p0 = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool kin = p0 + 256 * k < N;
+            o.rr[4 * k] = qa[j][k].x; o.rr[4 * k + 1] = qa[j][k].y; o.rr[4 * k + 2] = qa[j][k].z;
+            o.rr[4 * k + 3] = qa[j][k].w;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o.in[4 * k + e] = kin;
+        }
+        return o;
+    };
+    auto count_round = [&](int r) {  // pass 1's bookkeeping of round r (rd decoded)
         bad |= rd.bad;
         if (lane < kWaveParts) {
             int tw = 0;
@@ -1190,6 +1213,22 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
 #pragma unroll
                 for (int q = 0; q < kWaveParts; ++q) tw += lane == q ? rd.ptot[k][q] : 0;
             sl.tot[r][w][lane] = tw;
+        }
+    };
+    if (vec32) {  // pass 1: count
+        for (int r0 = 0; r0 < R; r0 += RB) {
+            load_batch(r0);
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+                if (r0 + j < R) {
+                    wave_round_decode(rd, raw_of(r0 + j, j), q0, vs, nrows, base);
+                    count_round(r0 + j);
+                }
+        }
+    } else {
+        for (int r = 0; r < R; ++r) {
+            wave_round_decode(rd, wave_round_load(r, w, t, idx, itype, tstride, N), q0, vs, nrows, base);
+            count_round(r);
         }
     }
     // out of range raises BoundsError; the workgroup of parts 0..3 reports it
@@ -1213,24 +1252,22 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     const bool direct = BIG && nrows > 0 && ((nrows - 1) >> vs) == 0;
     const bool G = BIG && !direct && total > kStepIndexMaxN;  // (uniform over the workgroup)
     WPH(1);
-    if (BIG && R > 1) cur = wave_round_load(R - 2, w, t, idx, itype, tstride, N);
-    for (int r = R - 1; r >= 0; --r) {  // pass 2: place (round R - 1 is still in registers)
-        if (r != R - 1) {
-            WaveRaw nxt;
-            if (r > 0) nxt = wave_round_load(r - 1, w, t, idx, itype, tstride, N);
-            wave_round_decode(rd, cur, q0, vs, nrows, base);
-            cur = nxt;
-        }
+    int run[kWaveParts];  // part q's positions in the rounds before this one
+#pragma unroll
+    for (int q = 0; q < kWaveParts; ++q) run[q] = 0;
+    auto place_round = [&](int r) {  // pass 2: round r (rd decoded) into the parts' regions
         int at0[kWaveParts];
 #pragma unroll
         for (int q = 0; q < kWaveParts; ++q) {
-            int before = 0;  // earlier rounds, then this round's earlier waves
-            for (int rr = 0; rr < r; ++rr)
+            int before = run[q], all = 0;  // earlier rounds, then this round's earlier waves
 #pragma unroll
-                for (int ww = 0; ww < kWaveParts; ++ww) before += sl.tot[rr][ww][q];
-#pragma unroll
-            for (int ww = 0; ww < kWaveParts; ++ww) before += ww < w ? sl.tot[r][ww][q] : 0;
+            for (int ww = 0; ww < kWaveParts; ++ww) {
+                const int c = sl.tot[r][ww][q];
+                before += ww < w ? c : 0;
+                all += c;
+            }
             at0[q] = (G || direct ? 0 : pbase[q]) + before;
+            run[q] += all;
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -1266,6 +1303,24 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
                     }
                 }
             }
+        }
+    };
+    if (!BIG) {
+        place_round(0);  // (one round: rd still holds it)
+    } else if (vec32) {
+        for (int r0 = 0; r0 < R; r0 += RB) {
+            load_batch(r0);
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+                if (r0 + j < R) {
+                    wave_round_decode(rd, raw_of(r0 + j, j), q0, vs, nrows, base);
+                    place_round(r0 + j);
+                }
+        }
+    } else {
+        for (int r = 0; r < R; ++r) {
+            wave_round_decode(rd, wave_round_load(r, w, t, idx, itype, tstride, N), q0, vs, nrows, base);
+            place_round(r);
         }
     }
     if (G) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

@@ -40,19 +40,22 @@ WORKLOADS = {
 
 
 WAVE_MAX_N = 16384  # the wave build's positions per table (csrc/common.hpp kWaveMaxN)
+APPLY_MAX_N = 2048   # where the in-apply wave build is the faster form
 
 
 def step_pipeline(w):
     """Where the training step's split indexer is built for workload `w` (the form bench.py times
     and tests/test_configs.py checks step by step on the CPU checker): "apply" = inside the previous
-    step's apply launch (one-hot batches <= 16384: the wave build, 16 parts per 2048 positions; the
-    forward then only gathers; round 3, metric config 49.1M vs 43.8M samples/s with the build in the
-    forward's launch), "side" = the next batch's build on a side stream (larger one-hot batches),
-    None = inside the forward's launch (pooled bags: the operator path, which builds its own)."""
+    step's apply launch (one-hot batches <= 2048: the forward then only gathers; round 3, metric
+    config 49.1M vs 43.8M samples/s with the build in the forward's launch), "side" = the next
+    batch's build on a side stream (one-hot batches > 2048: the in-LDS parts build; the in-apply wave
+    build takes up to 16384 positions per table but measured slower at 8192 -- 81 M vs 85 M samples/s
+    on configs[2], round 5), None = inside the forward's launch (pooled bags: the operator path, which
+    builds its own)."""
     L, B = w["lookups"], w["batch"]
     if L != 1:
         return None
-    return "apply" if B <= WAVE_MAX_N else "side"
+    return "apply" if B <= APPLY_MAX_N else "side"
 
 
 def table_bytes(rows, dim, esize):

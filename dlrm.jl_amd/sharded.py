@@ -141,10 +141,12 @@ class HipShardOps:
         self.ident = PackedIndices(ar.repeat(T, 1).reshape(T, Bm, 1))
 
     def build_indexer(self, idx):
-        """The update's split indexer over the global batch: the wave build (dlrm_indexer_prepare,
-        one-hot, <= 16384 positions per table: 16 parts per 2048 positions, one wave each) where it
-        applies, else dlrm_indexer_build (in-LDS or hash build)."""
-        if idx.L == 1 and self._prepare is not False:
+        """The update's split indexer over the global batch: the wave build (dlrm_indexer_prepare:
+        16 parts per table, one wave each) for one-hot global batches of <= 2048 positions per table
+        (configs[3] at global batch 2048: 11 us against the in-LDS build's 22 us), else
+        dlrm_indexer_build (in-LDS or hash build; at 16384 positions the wave build's 38 us did not
+        beat the hash build's 41 us)."""
+        if idx.L == 1 and idx.B <= 2048 and self._prepare is not False:
             rc = self.lib.dlrm_indexer_prepare(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
                                                idx.itype, idx.stride, self.base, idx.B)
             if rc == _lib.OK:
