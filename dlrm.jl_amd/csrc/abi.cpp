@@ -76,7 +76,8 @@ const Knobs& knobs() {
     static const Knobs k{env_int("DLRM_STEP_PARTS", 0),       env_int("DLRM_BUILD_PARTS", 0),
                          env_int("DLRM_RELU_2PASS", 1) == 0, env_int("DLRM_BWD_YS", 1) == 0,
                          env_int("DLRM_BWD_SPLIT", 1) == 0,  env_int("DLRM_BWD_SPB", 0),
-                         env_int("DLRM_BWD_CPL", 0),         env_int("DLRM_UPD_SBU", 1)};
+                         env_int("DLRM_BWD_CPL", 0),         env_int("DLRM_UPD_SBU", 1),
+                         env_int("DLRM_WAVE_ROUNDS", 0)};
     return k;
 }
 int ctx_device(dlrm_ctx* ctx) { return ctx->device; }

@@ -332,6 +332,8 @@ struct Knobs {
     int bwd_spb;      // DLRM_BWD_SPB (2/4/8): samples per block of the split step backward
     int bwd_cpl;      // DLRM_BWD_CPL (4/8): columns per lane of the bf16 split step backward
     int upd_sbu;      // DLRM_UPD_SBU (1/2): super-blocks in flight in the one-wave step backward
+    int wave_rounds;  // DLRM_WAVE_ROUNDS=1: the wave build in rounds above 2048 positions per table
+                      // instead of the scan build
 };
 const Knobs& knobs();
 

@@ -633,6 +633,7 @@ struct WaveBuildLds {
     // [round][wave][part]: positions of the workgroup's part q that wave w read in round r (a round
     // = 2048 positions, 512 per wave)
     int tot[kWaveMaxN / kStepIndexMaxN][kWaveParts][kWaveParts];
+    int4 wtot[16];  // the scan build: wave w's positions of the four parts
 };
 
 // The flat item lists come in kResLists sub-lists: build workgroup g reserves in sub-list g mod 8
@@ -921,7 +922,6 @@ template <bool G, bool DIRECT = false>
 __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
                                int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, int g, int groups) {
     const int lane = threadIdx.x & 63;
-    const unsigned long long lt = lanes_below();
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
     const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
     const int nbits = 32 - __clz(kmax);
@@ -1343,6 +1343,235 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
         wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb,
                               sl.R + pb, sl.cnt[w], g, groups);
     }
+}
+
+// The large-N builds' last step (after the workgroup barrier that follows the placement): wave w
+// sorts part q0 + w of table t -- n positions placed at pool offset pb, in HBM scratch (G), or
+// already in perm (direct).
+__device__ __forceinline__ void wave_build_sort(const IndexerDev& ix, int g, int T, int t, int q0, int vs,
+                                                uint32_t nrows, int n, int pb, bool direct, bool G,
+                                                WaveBuildLds& sl) {
+    const int w = threadIdx.x >> 6;
+    const int v = (t << vs) + q0 + w;
+    const int groups = (T << vs) / kWaveParts;
+    if (direct) {
+        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, sl.K[0] + 8 * w, sl.V[0] + 8 * w, sl.K[1] + 8 * w,
+                                    sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
+    } else if (G) {
+        uint32_t* K0 = ix.wscratch + (int64_t)v * ix.cap;
+        const int64_t S = ix.wstride;
+        wave_sort_part<true>(ix, v, t, vs, nrows, n, K0, (int32_t*)(K0 + S), K0 + 2 * S, (int32_t*)(K0 + 3 * S),
+                             (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
+    } else {
+        wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb,
+                              sl.R + pb, sl.cnt[w], g, groups);
+    }
+}
+
+// ---------------------------------------------------------------- scan wave build (N > 2048)
+// The one-launch build above 2048 positions per table without rounds: wave w of the workgroup's NW
+// (parts q0 .. q0 + 3 of table t) takes a contiguous 1 / NW of the table's positions, so the
+// parts' lists keep position order by (wave, piece, lane) offsets and the waves exchange nothing
+// but one count per part.  The quarter's indices are loaded once, all at once (pieces of 256
+// positions, one 16-B load per lane; <= 16 pieces = 64 registers at 16384 positions), and stay in
+// registers for two lean passes:
+//   1. count: per lane, this workgroup's positions per part in four 8-bit fields (<= 64 per lane),
+//      and a bit per position that is this workgroup's ("mine"); one wave reduction at the end;
+//   2. place: through a staging list when the four parts fit the LDS pool -- the wave's mine
+//      positions (~N / 32 at 128 parts) are appended in position order to its range of the pool's
+//      second array (part code in the top bits; one DPP scan per two pieces, of the lanes' mine
+//      counts), then split by part into their regions (two scans per 64 staged entries), so the
+//      per-part placement runs once per staged entry instead of once per piece; else (HBM scratch,
+//      or perm straight away for a table of <= P rows) by per-piece prefixes per part.
+// Every workgroup of a table still reads all N of its indices (from L2: 64 KB at 16384).  The scan
+// is a chain of dependent VALU / DPP steps, so more waves shorten it: the standalone build runs 16
+// waves per workgroup (4 per SIMD; waves 4 .. 15 leave before the sort), the in-apply build 4.  Needs
+// int32 indices, 16-B aligned per table, N % 4 == 0 (else the rounds form runs).
+template <int NW>
+__device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
+                                      const void* __restrict__ idx, int64_t tstride, int base, int N,
+                                      unsigned* __restrict__ err, WaveBuildLds& sl) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
+    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
+    const uint32_t pmask = (1u << vs) - 1u;
+    const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+    const int Q = ((N + NW * 256 - 1) / (NW * 256)) * 256;  // positions per wave (whole pieces)
+    const int pw0 = w * Q;
+    const int npc = pw0 < N ? (min(pw0 + Q, N) - pw0 + 255) / 256 : 0;  // this wave's pieces
+    constexpr int MP = kWaveMaxN / NW / 256;                          // (16 / NW = 4, 4 / NW = 16)
+    WPH(0);
+    int4 v[MP];
+#pragma unroll
+    for (int u = 0; u < MP; ++u) {
+        const int p = pw0 + 256 * u + 4 * lane;
+        if (u < npc && p < N) v[u] = ldg<int4>(i32 + p);
+    }
+    // pass 1: count
+    uint32_t acc = 0;
+    uint64_t mbits = 0;
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < MP; ++u) {
+        // (a guard, not a break: a loop with two exits is not unrolled, and v[] would go to scratch)
+        const bool in = u < npc && pw0 + 256 * u + 4 * lane < N;
+        const int xv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t x = (uint32_t)(xv[e] - base);
+            const bool ok = in && x < nrows;
+            bad |= in && !ok;
+            const uint32_t pq = (x & pmask) - (uint32_t)q0;
+            const bool m = ok && pq < (uint32_t)kWaveParts;
+            acc += m ? 1u << (8 * pq) : 0u;
+            mbits |= m ? 1ull << (4 * u + e) : 0ull;
+        }
+    }
+    if (q0 == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    {
+        const int a = (int)((acc & 0xffu) | (((acc >> 8) & 0xffu) << 16));
+        const int b = (int)(((acc >> 16) & 0xffu) | ((acc >> 24) << 16));
+        const int ta = lane63(wave_incl_scan(a)), tb = lane63(wave_incl_scan(b));
+        if (lane == 0) sl.wtot[w] = make_int4(ta & 0xffff, ta >> 16, tb & 0xffff, tb >> 16);
+    }
+    __syncthreads();
+    int n_of[kWaveParts], pbase[kWaveParts], at0[kWaveParts], total = 0, sbase = 0;
+    int4 nall = make_int4(0, 0, 0, 0), nbef = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+        const int4 c = sl.wtot[ww];
+        nall = make_int4(nall.x + c.x, nall.y + c.y, nall.z + c.z, nall.w + c.w);
+        if (ww < w) nbef = make_int4(nbef.x + c.x, nbef.y + c.y, nbef.z + c.z, nbef.w + c.w);
+    }
+#pragma unroll
+    for (int q = 0; q < kWaveParts; ++q) {
+        const int nq = q == 0 ? nall.x : (q == 1 ? nall.y : (q == 2 ? nall.z : nall.w));
+        const int before = q == 0 ? nbef.x : (q == 1 ? nbef.y : (q == 2 ? nbef.z : nbef.w));
+        n_of[q] = nq;
+        pbase[q] = total;
+        at0[q] = before;
+        sbase += before;
+        total += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
+    }
+    const bool direct = nrows > 0 && ((nrows - 1) >> vs) == 0;
+    const bool G = !direct && total > kStepIndexMaxN;  // (uniform over the workgroup)
+    WPH(1);
+    if (!G && !direct) {
+#pragma unroll
+        for (int q = 0; q < kWaveParts; ++q) at0[q] += pbase[q];
+        uint32_t* SK = sl.K[1];
+        int32_t* SV = sl.V[1];
+        int run = sbase;
+        auto stage = [&](const int4 vu, int u, int at) {  // (vu = v[u]: registers, u unrolled)
+            const int p = pw0 + 256 * u + 4 * lane;
+            const int xv[4] = {vu.x, vu.y, vu.z, vu.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if ((mbits >> (4 * u + e)) & 1ull) {
+                    const uint32_t x = (uint32_t)(xv[e] - base);
+                    SK[at] = x >> vs;
+                    SV[at] = (p + e) | (int)(((x & pmask) - (uint32_t)q0) << 28);
+                    ++at;
+                }
+        };
+#pragma unroll
+        for (int u = 0; u < MP; u += 2) {
+            if (u >= npc) continue;  // (uniform)
+            const int c0 = __popc((uint32_t)(mbits >> (4 * u)) & 15u);
+            const int c1 = u + 1 < npc ? __popc((uint32_t)(mbits >> (4 * u + 4)) & 15u) : 0;
+            const int pk = c0 | (c1 << 16);
+            const int incl = wave_incl_scan(pk), tot = lane63(incl);
+            const int ex = incl - pk;
+            stage(v[u], u, run + (ex & 0xffff));
+            if (u + 1 < npc) stage(v[u + 1], u + 1, run + (tot & 0xffff) + (ex >> 16));
+            run += (tot & 0xffff) + (tot >> 16);
+        }
+        wave_lds_sync();
+        for (int s0 = sbase; s0 < run; s0 += 64) {
+            const int s = s0 + lane;
+            const bool ok = s < run;
+            const uint32_t key = ok ? SK[s] : 0u;
+            const int32_t sv = ok ? SV[s] : 0;
+            const int q = ok ? (int)((uint32_t)sv >> 28) : 4;
+            const int a = (q == 0 ? 1 : 0) | (q == 1 ? 1 << 16 : 0), b = (q == 2 ? 1 : 0) | (q == 3 ? 1 << 16 : 0);
+            const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+            const int ta = lane63(ia), tb = lane63(ib);
+            const int pre[kWaveParts] = {(ia - a) & 0xffff, (ia - a) >> 16, (ib - b) & 0xffff, (ib - b) >> 16};
+            int dst = 0;
+#pragma unroll
+            for (int qq = 0; qq < kWaveParts; ++qq) dst = q == qq ? at0[qq] + pre[qq] : dst;
+            if (ok) {
+                sl.K[0][dst] = key;
+                sl.V[0][dst] = sv & 0x0fffffff;
+            }
+            at0[0] += ta & 0xffff;
+            at0[1] += ta >> 16;
+            at0[2] += tb & 0xffff;
+            at0[3] += tb >> 16;
+        }
+    } else {
+        // placed straight away (HBM scratch or perm: the staging list would not fit the pool; rare --
+        // a tiny table or hot rows -- so piece by piece, the indices reloaded from L2, which keeps the
+        // common path's registers free)
+#pragma unroll 1
+        for (int u = 0; u < npc; ++u) {
+            const int p = pw0 + 256 * u + 4 * lane;
+            int4 vu = make_int4(0, 0, 0, 0);
+            if (p < N) vu = ldg<int4>(i32 + p);
+            const int xv[4] = {vu.x, vu.y, vu.z, vu.w};
+            uint32_t rv[4], cd[4];
+            int cq[kWaveParts] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t x = (uint32_t)(xv[e] - base);
+                cd[e] = (mbits >> (4 * u + e)) & 1ull ? (x & pmask) - (uint32_t)q0 : 4u;
+                rv[e] = x >> vs;
+#pragma unroll
+                for (int q = 0; q < kWaveParts; ++q) cq[q] += cd[e] == (uint32_t)q ? 1 : 0;
+            }
+            const int a = cq[0] | (cq[1] << 16), b = cq[2] | (cq[3] << 16);
+            const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+            const int ta = lane63(ia), tb = lane63(ib);
+            int at[kWaveParts] = {at0[0] + ((ia - a) & 0xffff), at0[1] + ((ia - a) >> 16),
+                                  at0[2] + ((ib - b) & 0xffff), at0[3] + ((ib - b) >> 16)};
+            at0[0] += ta & 0xffff;
+            at0[1] += ta >> 16;
+            at0[2] += tb & 0xffff;
+            at0[3] += tb >> 16;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (cd[e] >= (uint32_t)kWaveParts) continue;
+                const int q = (int)cd[e];
+                int dst = 0, nq = 0;
+#pragma unroll
+                for (int x = 0; x < kWaveParts; ++x)
+                    if (q == x) {
+                        dst = at[x]++;
+                        nq = n_of[x];
+                    }
+                const int32_t pos = p + e;
+                const int64_t vo = (int64_t)((t << vs) + q0 + q) * ix.cap + dst;
+                if (direct) {  // the part's perm entry and the position's once-hit flag, now
+                    ix.perm[vo] = pos;
+                    ix.single[(int64_t)t * ix.cap + pos] = nq == 1 ? 1 : 0;
+                    if (dst < 8) {  // (the part's first positions: its chunk record carries 5 inline)
+                        sl.K[0][8 * q + dst] = rv[e];
+                        sl.V[0][8 * q + dst] = pos;
+                    }
+                } else {
+                    ix.wscratch[vo] = rv[e];
+                    ((int32_t*)ix.wscratch)[ix.wstride + vo] = pos;
+                }
+            }
+        }
+    }
+    if (G) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (G) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (w >= kWaveParts) return;  // (NW > 4: the extra waves only scanned; the sort has no barrier)
+    WPH(7);
+    wave_build_sort(ix, g, T, t, q0, vs, nrows, n_of[w], pbase[w], direct, G, sl);
 }
 
 }  // namespace dlrm

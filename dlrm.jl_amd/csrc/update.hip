@@ -356,11 +356,23 @@ __global__ __launch_bounds__(NT) void indexer_fast_kernel(IndexerDev ix, const T
 // balances, and no workgroup is launched past the work.
 // MODE 0: chunks + hot slices; 1: + once-hit (singles) items; 2: + the next batch's split indexer
 // in the first (pa.T << pa.ix.vshift) / 4 workgroups (PrepArgs); 3: the same for more than 2048
-// positions per table.
+// positions per table in rounds; 5: the same by the scan build.
 #ifndef DLRM_BUILD_PRIO
 #define DLRM_BUILD_PRIO 3
 #endif
 constexpr int kBuildPrio = DLRM_BUILD_PRIO;  // s_setprio of the in-apply build's waves (0..3)
+
+// The build of more than 2048 positions per table: 3 = the scan build (indexer.hpp
+// wave_build_group_scan; int32 indices, 16-B aligned per table, N % 4 == 0), the default; 1 = rounds
+// (wave_build_group<true>, any index type; DLRM_WAVE_ROUNDS=1 forces it).
+static int wave_big_kind(const PrepArgs& pa) {
+    if (knobs().wave_rounds) return 1;
+    const bool vec32 = pa.itype == DLRM_I32 && (uintptr_t)pa.idx % 16 == 0 && (pa.tstride * 4) % 16 == 0 &&
+                       pa.N % 4 == 0;
+    return vec32 ? 3 : 1;
+}
+// workgroups of a build (4 parts each)
+__host__ __device__ __forceinline__ int prep_groups(const PrepArgs& pa) { return (pa.T << pa.ix.vshift) / kWaveParts; }
 
 template <typename TT, typename GT, int VPR, int MODE>
 __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev ix, TableDesc* __restrict__ tabs, int T_,
@@ -372,17 +384,21 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     int bid = blockIdx.x, nblk = gridDim.x;
     if (MODE >= 2) {
         extern __shared__ __attribute__((aligned(16))) unsigned char prep_lds[];
-        const int NI = (pa.T << pa.ix.vshift) / kWaveParts;
+        const int NI = prep_groups(pa);
         if (bid < NI) {  // the next batch's split build: one wave per table part (indexer.hpp)
             // the build's waves first at the issue arbiter: its chain of dependent LDS / VALU steps is
             // the launch's longest, the apply waves beside it mostly wait on memory (A/B on one box:
             // 54.72 / 54.77 -> 54.91 / 55.04 M samples/s, apply 10.58 -> 10.45 us)
             __builtin_amdgcn_s_setprio(kBuildPrio);
             ITEM_START(4, 0, bid);
-            // (MODE 3: the build of more than 2048 positions per table -- rounds and the HBM overflow
-            // path -- in its own instantiation, so the step's MODE 2 kernel keeps its registers)
-            wave_build_group<MODE == 3>(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N,
-                                        pa.err, *(WaveBuildLds*)prep_lds);
+            // (MODE 3 / 5: the builds of more than 2048 positions per table, in their own
+            // instantiations, so the step's MODE 2 kernel keeps its registers)
+            if constexpr (MODE == 5)
+                wave_build_group_scan<kWaveParts>(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.tstride, pa.base, pa.N, pa.err,
+                                      *(WaveBuildLds*)prep_lds);
+            else
+                wave_build_group<MODE == 3>(pa.ix, bid, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base,
+                                            pa.N, pa.err, *(WaveBuildLds*)prep_lds);
             ITEM_END(0);
             return;
         }
@@ -531,24 +547,61 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
 }
 
 // The step indexer's workgroups alone (PrepArgs), where the apply has no vector kernel to host them.
+// KIND 0: one round (N <= 2048); 1: rounds (the scan build has its own kernel below).
+template <int KIND>
 __global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    if (pa.N <= kStepIndexMaxN)
-        wave_build_group<false>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
-                                *(WaveBuildLds*)lds);
-    else
-        wave_build_group<true>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N, pa.err,
-                               *(WaveBuildLds*)lds);
+    wave_build_group<KIND == 1>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.itype, pa.tstride, pa.base, pa.N,
+                                    pa.err, *(WaveBuildLds*)lds);
+}
+
+// The scan build alone (indexer.hpp wave_build_group_scan), NW waves per workgroup: 16 when every
+// workgroup is resident at once (one per CU: its ~94 registers allow 20 waves per CU), else 8 (two
+// per CU) -- a second round of workgroups would double the build.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void step_index_scan_kernel(PrepArgs pa) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    wave_build_group_scan<NW>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.tstride, pa.base, pa.N, pa.err,
+                              *(WaveBuildLds*)lds);
+}
+
+template <int NW>
+static void launch_step_index_scan(hipStream_t s, const PrepArgs& pa) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_scan_kernel<NW>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(WaveBuildLds));
+    (void)attr;
+    hipLaunchKernelGGL(step_index_scan_kernel<NW>, dim3((unsigned)prep_groups(pa)), dim3(64 * NW),
+                       sizeof(WaveBuildLds), s, pa);
+}
+
+static int pa_cus(const PrepArgs&) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    }
+    return cus;
+}
+
+template <int KIND>
+static void launch_step_index_kind(hipStream_t s, const PrepArgs& pa) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel<KIND>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(WaveBuildLds));
+    (void)attr;
+    hipLaunchKernelGGL(step_index_kernel<KIND>, dim3((unsigned)prep_groups(pa)), dim3(256),
+                       sizeof(WaveBuildLds), s, pa);
 }
 
 // step_index_kernel's own launch (the next batch's split build when the apply launch cannot carry it)
 static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_kernel,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)sizeof(WaveBuildLds));
-    (void)attr;
-    hipLaunchKernelGGL(step_index_kernel, dim3((unsigned)((pa.T << pa.ix.vshift) / kWaveParts)), dim3(256),
-                       sizeof(WaveBuildLds), s, pa);
+    const int kind = pa.N <= kStepIndexMaxN ? 0 : wave_big_kind(pa);
+    if (kind == 0) launch_step_index_kind<0>(s, pa);
+    else if (kind == 1) launch_step_index_kind<1>(s, pa);
+    else if (prep_groups(pa) <= pa_cus(pa)) launch_step_index_scan<16>(s, pa);
+    else launch_step_index_scan<8>(s, pa);
 }
 
 // The step's split build alone (dlrm_indexer_prepare): the wave build + item lists, 4 parts per
@@ -706,6 +759,19 @@ int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* t
     return ctx_hip(ctx, hipGetLastError(), "indexer_build launch");
 }
 
+// the apply launch that also carries the next batch's build (MODE >= 2): build workgroups first
+template <typename TT, typename GT, int VPR, int MODE>
+static void launch_apply_build(hipStream_t s, unsigned grid, const IndexerDev& ix, TableDesc* tabs, int T_, int L,
+                               const void* grad, int64_t grad_ld, int64_t grad_offset, float lr, const unsigned* err,
+                               const SinglesArgs& sa, const PrepArgs& pa) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, MODE>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(WaveBuildLds));
+    (void)attr;
+    hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, MODE>), dim3(grid), dim3(kApplyThreads), sizeof(WaveBuildLds), s,
+                       ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, pa);
+}
+
 template <typename TT, typename GT, int VPR>
 static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tabs, int T_, int L, const void* grad,
                              int64_t grad_ld, int64_t grad_offset, float lr, int64_t N, const unsigned* err,
@@ -731,23 +797,12 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     // (the once-hit items and the next batch's indexer are separate instantiations: the step's
     // apply stays lean)
     if (pa && !sa.single) {
-        static const hipError_t attr2 = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 2>,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                            (int)sizeof(WaveBuildLds));
-        static const hipError_t attr3 = hipFuncSetAttribute((const void*)sgd_apply_kernel<TT, GT, VPR, 3>,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                            (int)sizeof(WaveBuildLds));
-        (void)attr2;
-        (void)attr3;
-        const int NI = (pa->T << pa->ix.vshift) / kWaveParts;
-        if (pa->N <= kStepIndexMaxN)
-            hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 2>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
-                               sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
-                               sa, *pa);
-        else
-            hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 3>), dim3((unsigned)(grid + NI)), dim3(kApplyThreads),
-                               sizeof(WaveBuildLds), s, ix, tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err,
-                               sa, *pa);
+        // MODE 2: <= 2048 positions per table; above, 2 + wave_big_kind (3 rounds, 5 scan)
+        const int mode = pa->N <= kStepIndexMaxN ? 2 : 2 + wave_big_kind(*pa);
+        const unsigned g2 = (unsigned)(grid + prep_groups(*pa));
+        if (mode == 2) launch_apply_build<TT, GT, VPR, 2>(s, g2, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, err, sa, *pa);
+        else if (mode == 5) launch_apply_build<TT, GT, VPR, 5>(s, g2, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, err, sa, *pa);
+        else launch_apply_build<TT, GT, VPR, 3>(s, g2, ix, tabs, T_, L, grad, grad_ld, grad_offset, lr, err, sa, *pa);
     } else if (sa.single) {
         hipLaunchKernelGGL((sgd_apply_kernel<TT, GT, VPR, 1>), dim3((unsigned)grid), dim3(kApplyThreads), 0, s, ix,
                            tabs, T_, L, (const GT*)grad, grad_ld, grad_offset, lr, err, sa, PrepArgs{});

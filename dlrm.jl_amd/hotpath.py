@@ -31,6 +31,7 @@ from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices
 from .interact import interaction_sizes
 from .runtime import dtype_code, ptr, require_device
+from .shapes import APPLY_MAX_N
 from .update import SparseIndexer
 
 
@@ -83,6 +84,7 @@ class HotPath:
         if mode not in (None, "side", "apply"):
             raise ValueError(f"pipeline must be None, 'side' or 'apply', not {pipeline!r}")
         self.pipeline = mode if (mode and self.step_api and self.L == 1) else None
+        self._prepare_ok = None  # build_split: None untried, False the wave build does not take it
         if self.pipeline:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
             self._ix_of = [None, None]  # the PackedIndices each indexer was last built from
@@ -178,8 +180,20 @@ class HotPath:
                                            ptr(self.dt), self.dt.stride(0), self.lr, flags))
 
     def build_split(self, indexer, idx):
-        """dlrm_indexer_build_split: the indexer form dlrm_step_bwd consumes."""
+        """The indexer form dlrm_step_bwd consumes: the wave build (dlrm_indexer_prepare) for one-hot
+        batches of <= shapes.APPLY_MAX_N positions per table, else dlrm_indexer_build_split (the
+        in-LDS parts build up to 8192 positions, the hash build above: beside a step of B = 8192 the
+        parts build's 104 workgroups cost the step less than the wave build's 416)."""
         h = self.ctx.bind()
+        if idx.L == 1 and self.B <= APPLY_MAX_N and self._prepare_ok is not False:
+            rc = self.lib.dlrm_indexer_prepare(h, indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
+                                               idx.stride, self.index_base, self.B)
+            if rc == _lib.OK:
+                self._prepare_ok = True
+                return
+            if rc != _lib.E_UNSUPPORTED:
+                self._check(rc)
+            self._prepare_ok = False
         self._check(self.lib.dlrm_indexer_build_split(h, indexer.handle, self.ts.handle, ptr(idx.data), idx.itype,
                                                       idx.stride, self.index_base, self.B))
 

@@ -2,6 +2,8 @@
 
 Table row counts are the reference's own constants (src/data/criteo.jl:350-406).
 """
+import os
+
 import numpy as np
 
 # src/data/criteo.jl:350-377
@@ -40,7 +42,14 @@ WORKLOADS = {
 
 
 WAVE_MAX_N = 16384  # the wave build's positions per table (csrc/common.hpp kWaveMaxN)
-APPLY_MAX_N = 2048   # where the in-apply wave build is the faster form
+# One GPU: the in-apply wave build, and the side stream's wave build, up to APPLY_MAX_N positions per
+# table; above, the side stream's in-LDS parts build (configs[2] at 8192: 85.3 M samples/s, against
+# 69 M with the scan build in the apply launch and 82 M with it on the side stream, round 5).  The
+# sharded update's indexer: the wave build up to PREPARE_MAX_N (the scan build: 13.4 us for 4
+# tables x 16384 positions, against 40 us for the hash build).  DLRM_APPLY_MAX_N / DLRM_PREPARE_MAX_N
+# override, for A/B runs.
+APPLY_MAX_N = int(os.environ.get("DLRM_APPLY_MAX_N", 2048))
+PREPARE_MAX_N = int(os.environ.get("DLRM_PREPARE_MAX_N", WAVE_MAX_N))
 
 
 def step_pipeline(w):
@@ -49,9 +58,8 @@ def step_pipeline(w):
     step's apply launch (one-hot batches <= 2048: the forward then only gathers; round 3, metric
     config 49.1M vs 43.8M samples/s with the build in the forward's launch), "side" = the next
     batch's build on a side stream (one-hot batches > 2048: the in-LDS parts build; the in-apply wave
-    build takes up to 16384 positions per table but measured slower at 8192 -- 81 M vs 85 M samples/s
-    on configs[2], round 5), None = inside the forward's launch (pooled bags: the operator path, which
-    builds its own)."""
+    build takes up to 16384 positions per table but measured slower at 8192, APPLY_MAX_N), None =
+    inside the forward's launch (pooled bags: the operator path, which builds its own)."""
     L, B = w["lookups"], w["batch"]
     if L != 1:
         return None

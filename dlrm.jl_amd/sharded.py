@@ -55,7 +55,7 @@ from . import _lib
 from .embedding import EmbeddingTableSet, PackedIndices
 from .interact import interaction_sizes
 from .runtime import context, dtype_code, ptr
-from .shapes import zipf_perm, zipf_rows
+from .shapes import PREPARE_MAX_N, zipf_perm, zipf_rows
 from .update import SparseIndexer
 
 
@@ -142,11 +142,12 @@ class HipShardOps:
 
     def build_indexer(self, idx):
         """The update's split indexer over the global batch: the wave build (dlrm_indexer_prepare:
-        16 parts per table, one wave each) for one-hot global batches of <= 2048 positions per table
-        (configs[3] at global batch 2048: 11 us against the in-LDS build's 22 us), else
-        dlrm_indexer_build (in-LDS or hash build; at 16384 positions the wave build's 38 us did not
-        beat the hash build's 41 us)."""
-        if idx.L == 1 and idx.B <= 2048 and self._prepare is not False:
+        16 parts per 2048 positions per table, one wave each; above 2048 positions the scan build,
+        csrc/indexer.hpp wave_build_group_scan) for one-hot global batches of <= shapes.PREPARE_MAX_N
+        positions per table (world 8 at the metric config, 16384: 13.4 us against the hash build's
+        40 us; configs[3] at global batch 2048: 11 us against the in-LDS build's 22 us), else
+        dlrm_indexer_build (in-LDS or hash build)."""
+        if idx.L == 1 and idx.B <= PREPARE_MAX_N and self._prepare is not False:
             rc = self.lib.dlrm_indexer_prepare(self.ctx.bind(), self.indexer.handle, self.ts.handle, ptr(idx.data),
                                                idx.itype, idx.stride, self.base, idx.B)
             if rc == _lib.OK:

@@ -291,6 +291,23 @@ def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
     _assert_segments(ix, idx, B)
 
 
+@pytest.mark.parametrize("B,where,value", [(2049, -1, "over"), (8192, 5000, "negative"), (16384, 0, "over")])
+def test_wave_prepare_bounds(pkg, gpu, B, where, value):
+    """Above 2048 positions per table the prepared build partitions each 2048-position chunk by
+    part first (indexer.hpp wave_partition_chunk): an out-of-range index there (past the last row,
+    or negative; in the last, partial chunk too) raises BoundsError at the next check."""
+    rows = [3, 5000, 100000]
+    rng = np.random.default_rng(B)
+    idx = rand_indices(rng, rows, B, 1)
+    idx[1, where] = rows[1] if value == "over" else -1
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B, gpu)
+    tabs.ctx.check_bounds()
+    assert ix.prepare(tabs, torch.from_numpy(idx).to(torch.int32).to(gpu), index_base=0)
+    with pytest.raises(pkg.BoundsError):
+        tabs.ctx.check_bounds()
+
+
 def test_prepared_step_equals_fresh_step_and_bounds(pkg, gpu):
     """dlrm_indexer_prepare -> dlrm_step_fwd (gather only: the indexer is prepared) ->
     dlrm_step_bwd equals a step whose forward builds its own indexer, bit for bit; an out-of-range
