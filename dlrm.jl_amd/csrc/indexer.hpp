@@ -633,8 +633,10 @@ struct WaveBuildLds {
     // [round][wave][part]: positions of the workgroup's part q that wave w read in round r (a round
     // = 2048 positions, 512 per wave)
     int tot[kWaveMaxN / kStepIndexMaxN][kWaveParts][kWaveParts];
-    int4 wtot[16];  // the scan build: wave w's positions of the four parts
 };
+// the scan build's per-wave counts of its four parts (<= 16 waves), in the rounds form's tot array
+__device__ __forceinline__ int4* scan_wave_totals(WaveBuildLds& sl) { return (int4*)&sl.tot[0][0][0]; }
+static_assert(sizeof(WaveBuildLds::tot) >= 16 * sizeof(int4), "tot holds the scan build's wave totals");
 
 // The flat item lists come in kResLists sub-lists: build workgroup g reserves in sub-list g mod 8
 // (its XCD's), so each reservation word takes an eighth of the build's atomics (one word took ~2.7
@@ -1433,14 +1435,14 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
         const int a = (int)((acc & 0xffu) | (((acc >> 8) & 0xffu) << 16));
         const int b = (int)(((acc >> 16) & 0xffu) | ((acc >> 24) << 16));
         const int ta = lane63(wave_incl_scan(a)), tb = lane63(wave_incl_scan(b));
-        if (lane == 0) sl.wtot[w] = make_int4(ta & 0xffff, ta >> 16, tb & 0xffff, tb >> 16);
+        if (lane == 0) scan_wave_totals(sl)[w] = make_int4(ta & 0xffff, ta >> 16, tb & 0xffff, tb >> 16);
     }
     __syncthreads();
     int n_of[kWaveParts], pbase[kWaveParts], at0[kWaveParts], total = 0, sbase = 0;
     int4 nall = make_int4(0, 0, 0, 0), nbef = make_int4(0, 0, 0, 0);
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) {
-        const int4 c = sl.wtot[ww];
+        const int4 c = scan_wave_totals(sl)[ww];
         nall = make_int4(nall.x + c.x, nall.y + c.y, nall.z + c.z, nall.w + c.w);
         if (ww < w) nbef = make_int4(nbef.x + c.x, nbef.y + c.y, nbef.z + c.z, nbef.w + c.w);
     }
