@@ -273,11 +273,13 @@ def test_step_fwd_indexer_parts(pkg, gpu, rows, B, zipf):
     ([500, 2000, 1_000_000], 16384, 1.5, ""),                          # hot rows: multi-row parts in HBM
     ([1], 16384, None, ""), ([0x10000, 0x1000000], 3000, None, ""), ([7, 70000], 2049, None, ""),
     ([1000], 16384, None, "one-part"),                                 # every index in one part: 8 rows
-    ([5000, 3], 4100, 1.05, "")])
+    ([5000, 3], 4100, 1.05, ""),
+    ([300, 100000, 3, 5_000_000], 6000, 1.1, "int64")])               # int64 indices: the rounds form
 def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
-    """dlrm_indexer_prepare (the wave build: 16 parts per 2048 positions, rounds of 2048 positions,
-    parts that overflow a workgroup's LDS pool sorted in HBM) up to 16384 positions per table: unique
-    rows and per-row positions exactly numpy's, every once-hit flag right."""
+    """dlrm_indexer_prepare (the wave build: 16 parts per 2048 positions; above 2048 the scan build --
+    int32 indices, N % 4 == 0 -- else rounds of 2048 positions; parts that overflow a workgroup's LDS
+    pool sorted in HBM) up to 16384 positions per table: unique rows and per-row positions exactly
+    numpy's, every once-hit flag right."""
     if rows == "kaggle":
         rows = pkg.KAGGLE_EMBEDDING_SIZES
     rng = np.random.default_rng(B + len(rows) + 3)
@@ -286,7 +288,8 @@ def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
         idx = (5 + 128 * rng.integers(0, 7, size=(1, B))).astype(idx.dtype)
     tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B, gpu)
-    assert ix.prepare(tabs, torch.from_numpy(idx).to(torch.int32).to(gpu), index_base=0)
+    itype = torch.int64 if case == "int64" else torch.int32
+    assert ix.prepare(tabs, torch.from_numpy(idx).to(itype).to(gpu), index_base=0)
     tabs.ctx.check_bounds()
     _assert_segments(ix, idx, B)
 
@@ -1088,6 +1091,10 @@ SHARD_CASES = {
     "kaggle-scaled-d128": dict(rows=[1460, 583, 10131, 2202, 305, 24, 12517, 633, 3, 9314, 5683, 8351, 3194, 27,
                                      14992, 5461, 10, 5652, 2173, 4, 7046, 18, 15, 2861, 105, 1425],
                                D=128, B=128, L=1, zipf=None),
+    # global batch 4096 (> 2048 positions per table): the sharded update's indexer is the scan wave build
+    "kaggle-scaled-b4096": dict(rows=[1460, 583, 10131, 2202, 305, 24, 12517, 633, 3, 9314, 5683, 8351, 3194, 27,
+                                      14992, 5461, 10, 5652, 2173, 4, 7046, 18, 15, 2861, 105, 1425],
+                                D=32, B=2048, L=1, zipf=1.05),
 }
 
 
@@ -1152,7 +1159,7 @@ def _gpu_shard_worker(rank, world, port, outdir, owners=None, graphed=False, cas
 
 @pytest.mark.parametrize("owners,graphed,case,micro", [
     (None, False, "small", 1), ([[4, 0, 2], [1, 3]], True, "small", 1), ("fitting", True, "terabyte-scaled", 1),
-    (None, True, "kaggle-scaled-d128", 1),
+    (None, True, "kaggle-scaled-d128", 1), (None, True, "kaggle-scaled-b4096", 1),
     # micro-batches: exchange of one half overlapping the compute of the other (comm stream)
     (None, False, "small", 2), ([[4, 0, 2], [1, 3]], True, "small", 4), ("fitting", True, "terabyte-scaled", 2),
     (None, True, "kaggle-scaled-d128", 2)])
