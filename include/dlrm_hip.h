@@ -240,7 +240,9 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
 /* The training step's split build of `indices` on the ctx's stream -- a side stream: it depends on
  * the indices only -- so that the dlrm_step_fwd of the same indices only gathers (the build
  * dlrm_step_bwd_prepare runs inside an apply launch, as its own launch).  One-hot, batch <= 16384
- * positions per table (16 table parts per 2048 positions, one wave each), <= 31 tables; the indexer
+ * positions per table (16 table parts per 2048 positions, one wave each; above 2048 positions the
+ * scan build: 8 or 16 waves per workgroup scan the table, int32 indices with 16-B aligned tables and
+ * batch % 4 == 0, else the build in rounds), <= 31 tables; the indexer
  * must have been created for >= batch positions.  Replaces the SparseIndexer() build of
  * train.jl:276-281 ahead of the step (also the table-sharded update's build over the global
  * batch).  Out-of-range indices raise the ctx's bounds flag (and are left out of the build).
