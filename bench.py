@@ -8,7 +8,8 @@ with the dense vector x and dLoss/d(out) supplied as synthetic inputs already in
 Default workload (BASELINE metric): 26 Criteo-Kaggle tables (criteo.jl:350-377) x 128-dim
 fp32, 2048 samples per GPU, one-hot int32 indices drawn uniformly per table, 64 distinct
 batches cycled (their touched rows far exceed the 256 MiB Infinity Cache, so the timed gathers
-read HBM, not a warm MALL).  N > 1 (torchrun): tables sharded by table across ranks, per-GPU batch fixed
+read HBM, not a warm MALL).  N > 1 (under torchrun, or without a launcher: bench.py then starts one
+process per GPU itself): tables sharded by table across ranks, per-GPU batch fixed
 (weak scaling), RCCL all-to-all of the looked-up vectors forward and of their gradients
 backward (dlrm.jl_amd/sharded.py).  Rank 0 prints ONE JSON line.
 """
@@ -84,6 +85,54 @@ def parse():
                          "build; D=128 49.1M vs 43.8M samples/s with 0, D=16 72.6M), 1 for one-hot batches > 2048 "
                          "(configs[2] 73.8M vs 71.7M), 0 for pooled bags")
     return ap.parse_args()
+
+
+def rank_env(base, rank, world, port):
+    """The environment torchrun gives rank `rank` of a one-node job of `world` ranks."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(world, cmd, base_env=None, port=None, poll_s=0.05):
+    """`--gpus N` without a launcher (WORLD_SIZE unset): starts N fresh processes of `cmd`, one
+    per rank with torchrun's variables (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; rank r on
+    GPU r), before this process touches the GPU, and waits for them.  Returns the job's exit
+    code: 0 if every rank exits 0; else the first failing rank's code, after stopping the
+    others (a rank that dies leaves its peers blocked in a collective)."""
+    import subprocess
+    base_env = dict(os.environ if base_env is None else base_env)
+    port = port or free_port()
+    procs = [subprocess.Popen(cmd, env=rank_env(base_env, r, world, port)) for r in range(world)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
 
 
 def algorithmic_bytes(w, B, T, D, L, E, I, uniq, chunks, materialize_ys=True):
@@ -294,6 +343,14 @@ def load_prof(workload):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no outside launcher: one fresh process per rank, started before anything here touches the
+        # GPU (torch.cuda.device_count() does not initialise it on this stack)
+        backend = os.environ.get("DLRM_DIST_BACKEND", "nccl")
+        if backend == "nccl" and torch.cuda.device_count() < a.gpus:
+            raise SystemExit(f"--gpus {a.gpus}: only {torch.cuda.device_count()} GPU(s) visible (RCCL needs one "
+                             f"GPU per rank; DLRM_DIST_BACKEND=gloo rehearses ranks sharing one GPU)")
+        sys.exit(spawn_ranks(a.gpus, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]))
     pkg = dlrm_pkg.load()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -441,6 +498,8 @@ def main():
         for piece in plan(n):
             graphs[piece].replay()
 
+    local_ms = [0.0]  # this rank's ms per step in the last timed region
+
     def timed(n):
         # the W untimed warm-up steps run right before the region (the first warm-up pass above sits
         # behind graph capture and host work, which leave the GPU idle), then the pipelined indexer
@@ -460,6 +519,7 @@ def main():
         if world > 1:
             dist.barrier()
         ms = (time.perf_counter() - t0) * 1e3 / n
+        local_ms[0] = ms
         if world > 1:
             tt = torch.tensor([ms], device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -475,6 +535,25 @@ def main():
             print(json.dumps({"probe_region_ms_per_step": {n: v for n, v in res.items()}}))
         return
     ms = timed(a.steps)
+    dist_info = None
+    if world > 1:
+        # what the job ran on, as the collectives saw it: the rank count of an all-reduce over the
+        # default group (RCCL for backend "nccl"), the library communicator's own ncclCommCount when
+        # it carries the exchange, each rank's step time (value uses the max) and the table partition
+        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        one = torch.ones(1, device=cdev)
+        dist.all_reduce(one)
+        mine = torch.tensor([local_ms[0]], device=cdev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        E_ = 4 if w["dtype"] == "f32" else 2
+        dist_info = {"backend": dist.get_backend(), "ranks_in_allreduce": int(one.item()),
+                     "exchange": "abi" if engine.comm is not None else "torch.distributed all_to_all_single",
+                     "rccl_comm_nranks": engine.comm.nranks() if engine.comm is not None else None,
+                     "rank_ms_per_step": [round(float(t.item()), 4) for t in every],
+                     "partition": {"tables_per_rank": [list(o) for o in engine.part.owners],
+                                   "gb_per_rank": [round(b / 1e9, 2) for b in
+                                                   engine.part.bytes_per_rank(rows, D * E_)]}}
     # sustained: >= a.sustain seconds of back-to-back steps (whole cycles over the nb batches), so a
     # short K does not hide clock ramp or cache effects; reported beside value, not instead of it
     sustained = None
@@ -759,6 +838,7 @@ def main():
                                 if world == 1 and engine.pipeline else
                                 "dlrm_step_fwd/dlrm_step_bwd (indexer in the forward launch, once-hit rows "
                                 "updated in the backward)" if world == 1 and engine.step_api else "operators")},
+            **({"distributed": dist_info} if dist_info else {}),
             "sustained": sustained, "drop_in_chain": chain, "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -85,6 +85,7 @@ SIGNATURES = {
     "dlrm_indexer_read": (_i32, [_vp, _vp, _i32, _pi64, _pi64, _pi64, _pi64, _i64]),
     "dlrm_indexer_state": (_i32, [_vp, ctypes.POINTER(ctypes.c_uint)]),
     "dlrm_indexer_prepare": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32]),
+    "dlrm_indexer_bytes": (_i32, [_vp, _vp]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
     "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),
@@ -106,6 +107,7 @@ SIGNATURES = {
     "dlrm_comm_unique_id": (_i32, [_vp]),
     "dlrm_comm_init": (_i32, [_vp, _vp, _i32, _i32, _pp]),
     "dlrm_comm_destroy": (_i32, [_vp]),
+    "dlrm_comm_count": (_i32, [_vp, _vp]),
     "dlrm_alltoall_fwd": (_i32, [_vp, _vp, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
     "dlrm_alltoall_bwd": (_i32, [_vp, _vp, _i32, _i32, ctypes.POINTER(ctypes.c_int), _vp, _vp]),
     "dlrm_interact_bwd_blocked": (_i32, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp,

@@ -57,6 +57,12 @@ class CommExchange:
     def _counts(counts):
         return (ctypes.c_int * len(counts))(*[int(c) for c in counts])
 
+    def nranks(self):
+        """The rank count RCCL reports for this communicator (dlrm_comm_count = ncclCommCount)."""
+        n = ctypes.c_int(0)
+        _lib.check(self.lib.dlrm_comm_count(self.handle, ctypes.byref(n)))
+        return n.value
+
     def alltoall_fwd(self, send, recv, dim, batch_local, counts):
         """send [world][T_me][B][dim] -> recv [src][T_src][B][dim] (dtype of send)."""
         self.ctx.check(self.lib.dlrm_alltoall_fwd(self.ctx.bind(), self.handle, dtype_code(send.dtype), dim,

@@ -47,17 +47,19 @@ struct dlrm_indexer {
     int TV = 0;  // tables of the per-table arrays: 4T when the forward launch may split tables by row bits
     IndexerDev dev{};
     void* block = nullptr;  // one allocation for every array
+    size_t bytes = 0;       // its size
     void* partial_big = nullptr;  // partial rows for D > kPartialDim (allocated on first use)
     // recorded by the last build
     bool built = false;
     bool split = false;  // built by dlrm_step_fwd's kernel: once-hit rows are left to the backward
     bool prepared = false;  // built by dlrm_step_bwd_prepare for the next dlrm_step_fwd (not yet consumed)
     bool singles_done = false;  // a split backward has applied this build's once-hit rows already
-    // device word for the bounds errors of the NEXT batch's build inside an apply launch
-    // (dlrm_step_bwd_prepare): it must not be the ctx's flag, which that launch's apply items read to
-    // decide whether to write (a race); nothing reads it -- the next forward gathers the same
-    // indices and raises their errors on the ctx's flag.  (dlrm_indexer_prepare, its own launch,
-    // raises on the ctx's flag directly.)
+    // device words for the bounds errors of builds that may run beside a step's write-deciding
+    // kernels, which read the ctx's flag to decide whether to write (raising there would be a race,
+    // ADVICE r5): [0] dlrm_indexer_prepare (a side-stream build beside the current step; cleared
+    // before each build, folded into the ctx's flag by the apply of this indexer), [1] the NEXT
+    // batch's build inside an apply launch (dlrm_step_bwd_prepare; nothing reads it).  Either way the
+    // forward / lookup of the same indices raises their errors on the ctx's flag.
     unsigned* prep_err = nullptr;
     const void* indices = nullptr;
     int itype = 0, base = 0, B = 0, L = 0;
@@ -131,6 +133,7 @@ static void record_build(dlrm_indexer* ix, bool split, const void* indices, int 
     ix->prepared = false;
     ix->singles_done = false;
     ix->dev.has_map = 0;  // (set by dlrm_step_bwd_prepare, whose wave build writes the item map)
+    ix->dev.build_err = nullptr;  // (set by dlrm_indexer_prepare)
     ix->indices = indices;
     ix->itype = itype;
     ix->tstride = tstride;
@@ -580,6 +583,105 @@ int dlrm_interact_bwd_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* 
 }
 
 // --------------------------------------------------------------------------- indexer
+// Footprint.  The per-part arrays (perm, seg_start, seg_row, chunks, hot, hot_slice, hot_cnt: 92 B
+// per slot; + 20 B of HBM sort scratch above 2048 positions) hold `parts` virtual tables of cap
+// slots per table, because one part may receive every position of its table (a hot row).  An
+// indexer is created with the parts the builds up to 2048 positions use (16 per table, or fewer
+// for a smaller cap); a wave build of more positions (dlrm_indexer_prepare, dlrm_step_bwd_prepare:
+// 2^wave_vshift(N) parts, 128 at 16384) re-carves it with that many on first use -- outside graph
+// capture (26 tables at cap 16384 were ~7 GB per indexer from creation on, whether or
+// not a wave build ever ran).  Partial rows of multi-slice hot segments are per real table (the
+// wave build's item map indexes them by its flat slice number, at most pcap per table), times
+// the <= 8 parts of the builds without an item map.
+static int64_t partial_rows(const dlrm_indexer* ix) {
+    const int64_t T0 = ix->T > 0 ? ix->T : 1;
+    const int64_t cap = ix->dev.cap;
+    const int np = cap <= kPartsMaxN ? (indexer_parts(cap) < 8 ? indexer_parts(cap) : 8) : 1;
+    return T0 * np * ix->dev.pcap;
+}
+
+// (Re)carves every array of the indexer for `parts` virtual tables per table (contents reset).
+static int indexer_carve(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
+    const int64_t cap = ix->dev.cap;
+    const int64_t T0 = ix->T > 0 ? ix->T : 1;
+    const int64_t T = (int64_t)parts * T0;
+    const int64_t hs = ix->dev.hsize;
+    // carve every array out of one allocation (16-B aligned pieces)
+    struct Piece { void** p; size_t bytes; };
+    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1)), n0 = (size_t)(T0 * cap);
+    // the wave build's flat item lists: kResLists sub-lists of res_stride records (indexer.hpp), for
+    // the largest build this layout takes (T / 4 workgroups); the HBM sort scratch for cap > 2048
+    const size_t nrec = T >= 4 ? (size_t)kResLists * (size_t)res_stride((int)(T / 4), cap) + 64 : 64;
+    // (only the wave builds of > 2048 positions, which have > 16 parts, can sort in HBM)
+    const int64_t wstride = cap > kStepIndexMaxN && parts > (1 << 4) ? T * cap + 64 : 0;
+    IndexerDev d = ix->dev;
+    float* partial_keep = ix->partial_big ? d.partial : nullptr;  // (a grown partial buffer stays)
+    Piece pieces[] = {
+        {(void**)&d.keys0, n0 * 4},    {(void**)&d.keys1, n0 * 4},  {(void**)&d.vals0, n0 * 4},
+        {(void**)&d.vals1, n0 * 4},    {(void**)&d.perm, n * 4},    {(void**)&d.seg_start, n1 * 4},
+        {(void**)&d.seg_row, n * 4},   {(void**)&d.chunks, n * 32}, {(void**)&d.hot, n * 16},
+        {(void**)&d.hot_slice, n * 16}, {(void**)&d.hot_cnt, n * 4},
+        {(void**)&d.partial, partial_keep ? 0 : (size_t)partial_rows(ix) * kPartialDim * 4},
+        {(void**)&d.counts, (size_t)T * 32},   {(void**)&d.single, n0},
+        {(void**)&ix->prep_err, 16},
+        {(void**)&d.slice_rec, nrec * 32}, {(void**)&d.chunk_rec, nrec * 32},
+        {(void**)&d.wscratch, (size_t)wstride * 5 * 4},
+        {(void**)&d.item_tot, 64},     {(void**)&d.build_arrive, 2048},
+        // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
+        {(void**)&d.pslot, hs ? n0 * 4 : 0},   {(void**)&d.hent, (size_t)(T0 * hs) * 8},
+        {(void**)&d.hseg, (size_t)(T0 * hs) * 8},
+        {(void**)&d.hfill, (size_t)(T0 * hs) * 4}, {(void**)&d.hstate, hs ? (size_t)T0 * 32 : 0},
+    };
+    size_t total = 0;
+    for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
+    int rc = hip_set(ctx);
+    void* block = nullptr;
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMalloc(&block, total), "hipMalloc(indexer)");
+    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemset(block, 0, total), "hipMemset(indexer)");
+    char* base = (char*)block;
+    if (rc == DLRM_OK)
+        for (auto& pc : pieces) {
+            *pc.p = pc.bytes ? base : nullptr;
+            base += (pc.bytes + 255) & ~(size_t)255;
+        }
+    if (rc == DLRM_OK && hs)  // every slot starts empty (the alloc pass resets the slots it used)
+        rc = ctx_hip(ctx, hipMemset(d.hent, 0xff, (size_t)(T0 * hs) * 8), "hipMemset(hash slots)");
+    if (rc != DLRM_OK) {
+        if (block) (void)hipFree(block);
+        return rc;
+    }
+    if (partial_keep) d.partial = partial_keep;
+    d.wstride = wstride;
+    if (ix->block) {  // (nothing in flight may still read the old arrays)
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ix->block);
+    }
+    ix->block = block;
+    ix->dev = d;
+    ix->TV = (int)T;
+    ix->bytes = total;
+    ix->built = ix->prepared = ix->singles_done = false;
+    ix->dev.has_map = 0;
+    ix->dev.build_err = nullptr;
+    return DLRM_OK;
+}
+
+// The parts layout a wave build of `vs` (> 4: more than 2048 positions per table) needs, re-carved
+// on first use.  Refused while the ctx's stream is being captured (hipFree would break the capture):
+// run one step of that shape before capturing.
+static int ensure_parts(dlrm_ctx* ctx, dlrm_indexer* ix, int vs) {
+    if (has_parts(ix, vs)) return DLRM_OK;
+    if ((1 << vs) > indexer_parts(ix->dev.cap))
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "indexer of %lld positions per table: no %d-part layout",
+                        (long long)ix->dev.cap, 1 << vs);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(ctx->stream, &cs);
+    if (cs != hipStreamCaptureStatusNone)
+        return ctx_fail(ctx, DLRM_E_ARG, "the first wave build of > %d positions per table re-carves the indexer "
+                        "(%d parts per table): run it once before graph capture", kStepIndexMaxN, 1 << vs);
+    return indexer_carve(ctx, ix, 1 << vs);
+}
+
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm_indexer** out) {
     CHECK_ARG(ctx && out, "dlrm_indexer_create: null argument");
     *out = nullptr;
@@ -590,12 +692,6 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->ctx = ctx;
     ix->T = num_tables;
     const int64_t cap = max_lookups > 0 ? max_lookups : 1;
-    const int64_t T0 = num_tables > 0 ? num_tables : 1;
-    // the wave builds (N <= kWaveMaxN) and the parts build (N <= kPartsMaxN) sort each table as
-    // parts (by the low bits of the row): the per-table arrays then hold indexer_parts(cap) virtual
-    // tables per table (the hash arrays, single[] and the global sort scratch stay per real table)
-    const int64_t T = (int64_t)indexer_parts(cap) * T0;
-    ix->TV = (int)T;
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
     ix->dev.pdim = kPartialDim;
@@ -603,54 +699,21 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->dev.hsize = hs;
     ix->dev.hbits = 0;
     while (((int64_t)1 << ix->dev.hbits) < hs) ++ix->dev.hbits;
-    // carve every array out of one allocation (16-B aligned pieces)
-    struct Piece { void** p; size_t bytes; };
-    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1)), n0 = (size_t)(T0 * cap);
-    // the wave build's flat item lists: kResLists sub-lists of res_stride records (indexer.hpp), for
-    // the largest build this indexer takes (T / 4 workgroups); the HBM sort scratch for cap > 2048
-    const size_t nrec = T >= 4 ? (size_t)kResLists * (size_t)res_stride((int)(T / 4), cap) + 64 : 64;
-    const int64_t wstride = cap > kStepIndexMaxN && T > T0 ? T * cap + 64 : 0;
-    ix->dev.wstride = wstride;
-    Piece pieces[] = {
-        {(void**)&ix->dev.keys0, n0 * 4},    {(void**)&ix->dev.keys1, n0 * 4},  {(void**)&ix->dev.vals0, n0 * 4},
-        {(void**)&ix->dev.vals1, n0 * 4},    {(void**)&ix->dev.perm, n * 4},    {(void**)&ix->dev.seg_start, n1 * 4},
-        {(void**)&ix->dev.seg_row, n * 4},   {(void**)&ix->dev.chunks, n * 32}, {(void**)&ix->dev.hot, n * 16},
-        {(void**)&ix->dev.hot_slice, n * 16}, {(void**)&ix->dev.hot_cnt, n * 4},
-        {(void**)&ix->dev.partial, (size_t)T * (size_t)ix->dev.pcap * kPartialDim * 4},
-        {(void**)&ix->dev.counts, (size_t)T * 32},   {(void**)&ix->dev.single, n0},
-        {(void**)&ix->prep_err, 16},
-        {(void**)&ix->dev.slice_rec, nrec * 32}, {(void**)&ix->dev.chunk_rec, nrec * 32},
-        {(void**)&ix->dev.wscratch, (size_t)wstride * 5 * 4},
-        {(void**)&ix->dev.item_tot, 64},     {(void**)&ix->dev.build_arrive, 2048},
-        // hash indexer arrays (only when a build can exceed the in-LDS indexer's kFastMaxN)
-        {(void**)&ix->dev.pslot, hs ? n0 * 4 : 0},   {(void**)&ix->dev.hent, (size_t)(T0 * hs) * 8},
-        {(void**)&ix->dev.hseg, (size_t)(T0 * hs) * 8},
-        {(void**)&ix->dev.hfill, (size_t)(T0 * hs) * 4}, {(void**)&ix->dev.hstate, hs ? (size_t)T0 * 32 : 0},
-    };
-    size_t total = 0;
-    for (auto& pc : pieces) total += (pc.bytes + 255) & ~(size_t)255;
-    int rc = hip_set(ctx);
-    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMalloc(&ix->block, total), "hipMalloc(indexer)");
-    if (rc == DLRM_OK) rc = ctx_hip(ctx, hipMemset(ix->block, 0, total), "hipMemset(indexer)");
+    // the parts of the builds up to 2048 positions per table (16, or fewer for a smaller cap); the
+    // larger wave builds re-carve with more (ensure_parts)
+    const int parts = indexer_parts(cap) < (1 << 4) ? indexer_parts(cap) : (1 << 4);
+    const int rc = indexer_carve(ctx, ix, parts);
     if (rc != DLRM_OK) {
-        if (ix->block) (void)hipFree(ix->block);
         delete ix;
         return rc;
     }
-    char* base = (char*)ix->block;
-    for (auto& pc : pieces) {
-        *pc.p = pc.bytes ? base : nullptr;
-        base += (pc.bytes + 255) & ~(size_t)255;
-    }
-    if (hs) {  // every slot starts empty (the alloc pass resets the slots it used)
-        rc = ctx_hip(ctx, hipMemset(ix->dev.hent, 0xff, (size_t)(T0 * hs) * 8), "hipMemset(hash slots)");
-        if (rc != DLRM_OK) {
-            (void)hipFree(ix->block);
-            delete ix;
-            return rc;
-        }
-    }
     *out = ix;
+    return DLRM_OK;
+}
+
+int dlrm_indexer_bytes(const dlrm_indexer* ix, int64_t* bytes) {
+    if (!ix || !bytes) return DLRM_E_ARG;
+    *bytes = (int64_t)ix->bytes + (ix->partial_big ? partial_rows(ix) * (int64_t)ix->dev.pdim * 4 : 0);
     return DLRM_OK;
 }
 
@@ -714,19 +777,27 @@ int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb,
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_prepare: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_prepare: batch %d > capacity %lld", batch, (long long)ix->dev.cap);
     const int vs = wave_parts_log2(batch);
-    if (batch > kWaveMaxN || tb->T + 1 > 32 || !has_parts(ix, vs))
+    if (batch > kWaveMaxN || tb->T + 1 > 32 || (1 << vs) > indexer_parts(ix->dev.cap))
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d, %d tables (the wave build: batch <= %d, "
                         "<= 31 tables)", batch, tb->T, kWaveMaxN);
+    rc = ensure_parts(ctx, ix, vs);
+    if (rc) return rc;
     ix->built = false;
     ix->prepared = false;
     ix->dev.vshift = vs;
-    // (its own launch: bounds errors go to the ctx's flag, as the lookup of the same indices raises them)
+    // bounds errors go to the indexer's own word, not the ctx's flag: this build usually runs on a
+    // side stream beside the current step, whose kernels read the ctx's flag to decide whether to
+    // write their rows.  The next forward / lookup of these indices raises them on the ctx's flag;
+    // the apply of this indexer folds the word in as well (a prebuilt update without a lookup).
+    rc = ctx_hip(ctx, hipMemsetAsync(ix->prep_err, 0, sizeof(unsigned), ctx->stream), "clear build bounds word");
+    if (rc) return rc;
     rc = launch_step_prepare(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
-                             ctx->err);
+                             ix->prep_err);
     if (rc) return rc;
     record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
     ix->prepared = true;
     ix->dev.has_map = 1;
+    ix->dev.build_err = ix->prep_err;
     return DLRM_OK;
 }
 
@@ -807,8 +878,7 @@ static int ensure_partials(dlrm_ctx* ctx, dlrm_indexer* ix, int D) {
     void* p = nullptr;
     int rc = hip_set(ctx);
     if (rc == DLRM_OK)
-        rc = ctx_hip(ctx, hipMalloc(&p, (size_t)ix->TV * (size_t)ix->dev.pcap * D * 4),
-                     "hipMalloc(indexer partials)");
+        rc = ctx_hip(ctx, hipMalloc(&p, (size_t)partial_rows(ix) * D * 4), "hipMalloc(indexer partials)");
     if (rc) return rc;
     if (ix->partial_big) (void)hipFree(ix->partial_big);
     ix->partial_big = p;
@@ -1008,7 +1078,7 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     const int NB = (tb->T + 1 + 15) / 16;
     // (the split backward's shapes only: the apply launch that carries the build has no once-hit items)
     const bool inapply = batch > 0 && tb->T > 0 && batch <= kWaveMaxN && NB <= 2 && tb->aligned16 &&
-                         has_parts(next, wave_parts_log2(batch)) &&
+                         (1 << wave_parts_log2(batch)) <= indexer_parts(next->dev.cap) &&
                          step_split_supported(tb->aligned16, tb->T, tb->dtype, tb->D, x, x_ld);
     if (!inapply)  // no pipelined form for this shape: the plain step (the next forward builds)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
@@ -1016,13 +1086,15 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     if (flags & DLRM_STEP_BWD_ONLY)  // (the next build rides on the apply launch)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
+    rc = ensure_parts(ctx, next, wave_parts_log2(batch) < 2 ? 2 : wave_parts_log2(batch));
+    if (rc) return rc;
     next->built = false;
     next->prepared = false;
     // the wave build: 2^wave_parts_log2(batch) parts per table, one wave each (4 per workgroup)
     next->dev.vshift = wave_parts_log2(batch);
     if (next->dev.vshift < 2) next->dev.vshift = 2;
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
-                      next->prep_err};
+                      next->prep_err + 1};
     rc = step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld, padding,
                        dx, dx_ld, dt, dt_ld, lr, flags, &pa);
     if (rc) return rc;

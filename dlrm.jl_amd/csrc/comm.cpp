@@ -103,6 +103,14 @@ int dlrm_comm_destroy(dlrm_comm* comm) {
     return DLRM_OK;
 }
 
+int dlrm_comm_count(const dlrm_comm* comm, int* nranks) {
+    if (!comm || !nranks || !comm->nccl) return DLRM_E_ARG;
+    int n = 0;
+    if (ncclCommCount(comm->nccl, &n) != ncclSuccess) return DLRM_E_HIP;
+    *nranks = n;
+    return DLRM_OK;
+}
+
 int dlrm_alltoall_fwd(dlrm_ctx* ctx, dlrm_comm* comm, int dtype, int dim, int batch_local,
                       const int* table_counts, const void* send, void* recv) {
     if (!ctx) return DLRM_E_ARG;

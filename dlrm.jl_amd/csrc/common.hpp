@@ -300,6 +300,10 @@ struct IndexerDev {
     int64_t wstride;
     int32_t* item_tot;
     uint32_t* build_arrive;  // the reservation words (64 bits, 256 B apart)
+    // the bounds word of a standalone prepared build (dlrm_indexer_prepare), or null: the apply of
+    // this indexer folds it into the ctx's flag (its lookups raise the same errors; this covers a
+    // prebuilt update without one)
+    const unsigned* build_err;
     int has_map;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)

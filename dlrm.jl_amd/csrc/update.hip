@@ -412,7 +412,12 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
     // this step): the reference's gather throws before update!, so no table row is written.  (The
     // error word is loaded with the item counts, one round trip for both.)
     const FastDiv Ld(L);  // position -> bag
-    const unsigned err0 = ldg<unsigned>(err);
+    unsigned err0 = ldg<unsigned>(err);
+    if (ix.build_err) {  // a standalone prepared build's out-of-range indices (written by an earlier launch)
+        const unsigned be = ldg<unsigned>(ix.build_err);
+        if (be && !err0 && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) raise_index_error((unsigned*)err);
+        err0 |= be;
+    }
     typedef ApplyGeom<GT, VPR> G;
     constexpr int D = G::D, NG = G::NG;
     __shared__ SliceLds<D> sm;
@@ -619,6 +624,10 @@ template <typename TT, typename GT>
 __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDesc* __restrict__ tabs, int D, int L,
                                                          const GT* __restrict__ grad, int64_t grad_ld,
                                                          int64_t grad_offset, float lr, const unsigned* __restrict__ err) {
+    if (ix.build_err && *ix.build_err) {  // (a prepared build's bounds error: raised here, before hot / singles)
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) raise_index_error((unsigned*)err);
+        return;
+    }
     if (*err) return;
     const int t = blockIdx.y;
     const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];

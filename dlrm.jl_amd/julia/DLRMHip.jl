@@ -107,6 +107,10 @@ function upload!(m::DeviceMatrix{T}, src::AbstractMatrix{T}) where {T}
     return m
 end
 function Base.Array(m::DeviceMatrix{T}) where {T}
+    # a host read of any buffer of the context (e.g. Array(tables[t].data)) sees every update! made
+    # so far: deferred apply launches of its table sets run first (update! writes the tables in
+    # place before it returns in the reference, train.jl:283-290)
+    flush_ctx!(m.ctx)
     dst = Matrix{T}(undef, size(m))
     check(m.ctx, ccall((:dlrm_memcpy_d2h, libdlrm), Cint, (Ptr{Cvoid}, Ptr{T}, Ptr{Cvoid}, Csize_t),
                        m.ctx.ptr, dst, m.ptr, sizeof(dst)))
@@ -191,6 +195,10 @@ prealloc_rows(s::PreallocationStrategy) =
 function _maplookup(tables::AbstractVector{<:HipEmbedding{Static{D},T}}, sparse, P::Integer) where {D,T}
     ctx = first(tables).data.ctx
     idx = sparse isa PackedIndices ? sparse : pack(ctx, sparse)
+    # every entry point that reads the tables applies a deferred update! first (the DefaultStrategy
+    # method, HipLookup's DeviceMatrix, the unfused rrule), as _fused_maplookup does
+    poll_bounds!(tables)
+    flush!(tables)
     ys = DeviceMatrix{T}(ctx, P + D * length(tables), idx.batch)
     check(ctx, ccall((:dlrm_maplookup, libdlrm), Cint,
                      (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, Cint, Cint, Cint, Ptr{Cvoid}, Int64, Int64),
@@ -548,6 +556,15 @@ function flush!(tables; next = nothing)
     return nothing
 end
 
+# every deferred update! whose tables live on ctx (a host-visible read point: Array of any of its
+# buffers)
+function flush_ctx!(ctx::Context)
+    for (tables, st) in collect(CHAIN_PENDING)
+        st.ctx === ctx && flush!(tables)
+    end
+    return nothing
+end
+
 """
     poll_bounds!(tables)
 
@@ -714,6 +731,13 @@ function comm_unique_id()
     rc = ccall((:dlrm_comm_unique_id, libdlrm), Cint, (Ptr{UInt8},), id)
     rc == 0 || throw(DLRMError(rc, "dlrm_comm_unique_id"))
     return id
+end
+"The rank count RCCL reports for the communicator (ncclCommCount)."
+function nranks(c::Comm)
+    n = Ref{Cint}(0)
+    rc = ccall((:dlrm_comm_count, libdlrm), Cint, (Ptr{Cvoid}, Ref{Cint}), c.ptr, n)
+    rc == 0 || throw(DLRMError(rc, "dlrm_comm_count"))
+    return Int(n[])
 end
 alltoall_fwd!(c::Comm, send::DeviceMatrix{T}, recv::DeviceMatrix{T}, D::Integer, B::Integer) where {T} =
     check(c.ctx, ccall((:dlrm_alltoall_fwd, libdlrm), Cint,

@@ -129,6 +129,12 @@ class SparseIndexer:
         self._built_from = idx
         return True
 
+    def nbytes(self):
+        """Device bytes held (dlrm_indexer_bytes: grows on the first wave build of > 2048 positions)."""
+        b = ctypes.c_int64()
+        self.ctx.check(self.ctx.lib.dlrm_indexer_bytes(self.handle, ctypes.byref(b)))
+        return b.value
+
     def state(self):
         """Host-side state of the last build: a mask of _lib.IX_* bits (no GPU call)."""
         st = ctypes.c_uint()

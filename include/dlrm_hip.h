@@ -245,10 +245,21 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
  * batch % 4 == 0, else the build in rounds), <= 31 tables; the indexer
  * must have been created for >= batch positions.  Replaces the SparseIndexer() build of
  * train.jl:276-281 ahead of the step (also the table-sharded update's build over the global
- * batch).  Out-of-range indices raise the ctx's bounds flag (and are left out of the build).
- * DLRM_E_UNSUPPORTED: a shape the wave build does not take (use dlrm_indexer_build). */
+ * batch).  Out-of-range indices are left out of the build and raise the ctx's bounds flag through
+ * the lookup / forward of the same indices, or the apply of this indexer (dlrm_sgd_update PREBUILT,
+ * dlrm_step_bwd) -- not from the build itself, which may run beside a step that reads the flag to
+ * decide its writes.  DLRM_E_UNSUPPORTED: a shape the wave build does not take (use
+ * dlrm_indexer_build). */
 int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
                          const void* indices, int itype, int64_t table_stride, int index_base, int batch);
+
+/* Device bytes the indexer holds.  It is created with the per-part arrays of the builds up to 2048
+ * positions per table (16 parts per table: ~92 B x 16 x cap per table, plus the item lists and, above
+ * 4096, the hash arrays); the first wave build of more positions (dlrm_indexer_prepare,
+ * dlrm_step_bwd_prepare; 2^k parts per table, 16 per 2048 positions) re-carves it with that many
+ * parts -- ~112 B x 128 x 16384 = 235 MB per table at 16384 positions -- so run one such build
+ * before graph capture (inside a capture it returns DLRM_E_ARG). */
+int dlrm_indexer_bytes(const dlrm_indexer* indexer, int64_t* bytes);
 
 /* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
  * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only
@@ -349,6 +360,8 @@ typedef struct dlrm_comm dlrm_comm;
 int dlrm_comm_unique_id(void* id);
 int dlrm_comm_init(dlrm_ctx* ctx, const void* id, int rank, int nranks, dlrm_comm** out);
 int dlrm_comm_destroy(dlrm_comm* comm);
+/* the rank count RCCL reports for the communicator (ncclCommCount), into *nranks */
+int dlrm_comm_count(const dlrm_comm* comm, int* nranks);
 int dlrm_alltoall_fwd(dlrm_ctx* ctx, dlrm_comm* comm, int dtype, int dim, int batch_local, const int* table_counts,
                       const void* send, void* recv);
 int dlrm_alltoall_bwd(dlrm_ctx* ctx, dlrm_comm* comm, int dim, int batch_local, const int* table_counts,

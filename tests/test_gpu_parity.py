@@ -294,21 +294,79 @@ def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
     _assert_segments(ix, idx, B)
 
 
-@pytest.mark.parametrize("B,where,value", [(2049, -1, "over"), (8192, 5000, "negative"), (16384, 0, "over")])
-def test_wave_prepare_bounds(pkg, gpu, B, where, value):
-    """Above 2048 positions per table the prepared build partitions each 2048-position chunk by
-    part first (indexer.hpp wave_partition_chunk): an out-of-range index there (past the last row,
-    or negative; in the last, partial chunk too) raises BoundsError at the next check."""
-    rows = [3, 5000, 100000]
-    rng = np.random.default_rng(B)
-    idx = rand_indices(rng, rows, B, 1)
-    idx[1, where] = rows[1] if value == "over" else -1
-    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+@pytest.mark.parametrize("rows,B,table,where,value,itype,zipf", [
+    ([3, 5000, 100000], 2048, 1, 77, "over", torch.int32, None),        # one round (N <= 2048)
+    ([3, 5000, 100000], 2049, 1, -1, "over", torch.int32, None),        # rounds (N % 4 != 0), last chunk
+    ([3, 5000, 100000], 8192, 1, 5000, "negative", torch.int32, None),  # the scan build
+    ([3, 5000, 100000], 16384, 1, 0, "over", torch.int32, None),
+    ([300, 100000, 3, 5_000_000], 6000, 3, 4321, "over", torch.int64, None),  # int64: the rounds form
+    ([3, 5000], 4100, 0, 17, "over", torch.int32, None),               # a tiny table: DIRECT parts
+    ([500, 2000, 1_000_000], 16384, 0, 9000, "negative", torch.int32, 1.5),  # hot rows: parts in HBM (G)
+])
+def test_wave_prepare_bounds(pkg, gpu, rows, B, table, where, value, itype, zipf):
+    """dlrm_indexer_prepare with an out-of-range index (past the last row, or negative) in every
+    form of the wave build: wave_build_group (one round, rounds, int64), wave_build_group_scan,
+    a DIRECT tiny table, a workgroup sorting in HBM (G).  ADVICE r5: the build itself does not
+    raise the ctx's flag (it may run beside a step whose kernels read that flag to decide their
+    writes); the apply of the prepared indexer (a prebuilt update_) raises BoundsError and writes
+    no row.  The word is cleared by the next prepare: a clean batch then updates normally."""
+    rng = np.random.default_rng(B + table)
+    idx = rand_indices(rng, rows, B, 1, zipf=zipf)
+    good = idx.copy()
+    idx[table, where] = rows[table] if value == "over" else -1
+    D = 16
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, D), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B, gpu)
     tabs.ctx.check_bounds()
-    assert ix.prepare(tabs, torch.from_numpy(idx).to(torch.int32).to(gpu), index_base=0)
+    bad = torch.from_numpy(idx).to(itype).to(gpu)
+    assert ix.prepare(tabs, bad, index_base=0)
+    tabs.ctx.check_bounds()  # (no raise: the build leaves the ctx's flag alone)
+    dy = torch.ones((B, len(rows) * D), device=gpu)
+    grads = pkg.maplookup_pullback(0, tabs, bad, dy)
     with pytest.raises(pkg.BoundsError):
-        tabs.ctx.check_bounds()
+        pkg.update_(pkg.Descent(0.5), tabs, grads, ix, index_base=0, prebuilt=True)
+    for t in tabs:
+        assert not t.data.any()  # no row written
+    ok = torch.from_numpy(good).to(itype).to(gpu)
+    assert ix.prepare(tabs, ok, index_base=0)
+    pkg.update_(pkg.Descent(0.5), tabs, pkg.maplookup_pullback(0, tabs, ok, dy), ix, index_base=0, prebuilt=True)
+    for t, n in enumerate(rows):
+        cnt = np.bincount(good[t], minlength=n).astype(np.float32)
+        assert np.array_equal(to_np_f32(tabs[t].data), np.repeat(-0.5 * cnt[:, None], D, axis=1))
+
+
+def test_step_next_bad_index_in_next_batch_only(pkg, gpu):
+    """HotPath.step_next builds the NEXT batch's indexer on a side stream beside the
+    current step.  An out-of-range index in that next batch must not freeze the current step (its
+    once-hit rows are written by the backward, which reads the ctx's flag): the current step's
+    tables equal a plain step bit for bit and no BoundsError is raised yet; the next step raises it
+    and writes nothing."""
+    rows, D, B = [3, 40, 100000, 7, 2_000_000], 64, 2048
+    rng = np.random.default_rng(5)
+    tabs = rand_tables(rng, rows, D)
+    good_np = rand_indices(rng, rows, B, 1)
+    bad_np = rand_indices(rng, rows, B, 1)
+    bad_np[2, 1234] = rows[2] + 1
+    good = pkg.PackedIndices(torch.from_numpy(good_np).to(torch.int32).to(gpu))
+    bad = pkg.PackedIndices(torch.from_numpy(bad_np).to(torch.int32).to(gpu))
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = len(rows) + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0, pipeline="side")
+    hp.step_next(x, good, dout, bad)
+    torch.cuda.synchronize()
+    hp.check_bounds()  # the bad batch has not been looked up yet
+    ref = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=0.25, index_base=0)
+    ref.step(x, good, dout)
+    torch.cuda.synchronize()
+    for a, b in zip(hp.ts, ref.ts):
+        assert torch.equal(a.data, b.data)
+    before = [t.data.clone() for t in hp.ts]
+    hp.step_next(x, bad, dout, good)
+    with pytest.raises(pkg.BoundsError):
+        hp.check_bounds()
+    for a, b in zip(hp.ts, before):
+        assert torch.equal(a.data, b)
 
 
 def test_prepared_step_equals_fresh_step_and_bounds(pkg, gpu):
@@ -809,6 +867,42 @@ def test_drop_in_chain_deferred_update(pkg, gpu):
     for a, b in zip(got, hp.ts):
         assert np.array_equal(a, to_np_f32(b.data))
     ht.hotpath(B).check_bounds()
+
+
+def test_default_strategy_lookup_after_a_deferred_update(pkg, gpu):
+    """a DefaultStrategy maplookup (test/model/embedding_update.jl:31) right after a
+    deferred update! must see that update applied, as the reference's update! writes the tables in
+    place before it returns (train.jl:283-290).  The Julia shim flushes in _maplookup; the Python
+    mirror through HipTables.ts.  Checked against the same steps on HotPath, bit for bit."""
+    rows, D, B = [3, 50, 1000, 100000], 16, 256
+    rng = np.random.default_rng(7)
+    T = len(rows)
+    tabs = [rng.uniform(-0.05, 0.05, size=(n, D)).astype(np.float32) for n in rows]
+    idxs = [pkg.PackedIndices(torch.from_numpy(rand_indices(rng, rows, B, 1)).to(torch.int32).to(gpu))
+            for _ in range(2)]
+    x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu)
+    F = T + 1
+    dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
+    lr = 0.5
+    ht = pkg.HipTables(dev_tables(tabs, gpu), lr=lr, index_base=0)
+    dot = pkg.DotInteraction()
+    for p in idxs:
+        ys = pkg.maplookup(pkg.PreallocationStrategy(D), ht, p)
+        _, back = pkg.rrule(dot, x, ys)
+        _, _, dy = back(dout)
+        pkg.update_(pkg.Descent(lr), ht, pkg.maplookup_pullback(D, ht, p, dy), pkg.SparseIndexer(T, B, gpu),
+                    num_splits=8, nthreads=12)
+    assert ht._pending is not None  # deferred
+    got = pkg.maplookup(pkg.DefaultStrategy(), ht, idxs[0])
+    assert ht._pending is None
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu)), B, 1, lr=lr, index_base=0)
+    for p in idxs:
+        hp.step(x, p, dout)
+    torch.cuda.synchronize()
+    i0 = idxs[0].data.reshape(T, B).cpu().numpy()
+    for t in range(T):
+        want = to_np_f32(hp.ts[t].data)[i0[t]]
+        assert np.array_equal(to_np_f32(got[t]), want)
 
 
 @pytest.mark.parametrize("sync_before_next", [True, False])
