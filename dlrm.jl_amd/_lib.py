@@ -51,6 +51,7 @@ SIGNATURES = {
     "dlrm_ctx_destroy": (_i32, [_vp]),
     "dlrm_ctx_set_stream": (_i32, [_vp, _vp]),
     "dlrm_last_error": (ctypes.c_char_p, [_vp]),
+    "dlrm_debug_fatal_trace": (_i32, [_i32]),
     "dlrm_sync": (_i32, [_vp]),
     "dlrm_check_bounds": (_i32, [_vp]),
     "dlrm_error_snapshot": (_i32, [_vp]),
@@ -86,6 +87,7 @@ SIGNATURES = {
     "dlrm_indexer_state": (_i32, [_vp, ctypes.POINTER(ctypes.c_uint)]),
     "dlrm_indexer_prepare": (_i32, [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32]),
     "dlrm_indexer_bytes": (_i32, [_vp, _vp]),
+    "dlrm_indexer_reserve": (_i32, [_vp, _vp, _i32]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
     "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),

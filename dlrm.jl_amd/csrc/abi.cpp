@@ -3,7 +3,11 @@
 // Owns the three handle types (ctx, tables, indexer), validates arguments on the host,
 // maps HIP errors to dlrm_status codes and forwards to the kernel launchers.  No launching
 // entry point allocates or synchronises (hipGraph-capturable).
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <cstdarg>
 #include <cstdio>
@@ -711,6 +715,14 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     return DLRM_OK;
 }
 
+int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* ix, int batch) {
+    CHECK_ARG(ctx && ix, "dlrm_indexer_reserve: null argument");
+    CHECK_ARG(batch >= 0 && batch <= ix->dev.cap, "dlrm_indexer_reserve: batch %d > capacity %lld", batch,
+              (long long)ix->dev.cap);
+    if (batch <= kStepIndexMaxN || batch > kWaveMaxN || ix->T == 0) return DLRM_OK;  // (nothing to re-carve)
+    return ensure_parts(ctx, ix, wave_parts_log2(batch));
+}
+
 int dlrm_indexer_bytes(const dlrm_indexer* ix, int64_t* bytes) {
     if (!ix || !bytes) return DLRM_E_ARG;
     *bytes = (int64_t)ix->bytes + (ix->partial_big ? partial_rows(ix) * (int64_t)ix->dev.pdim * 4 : 0);
@@ -1101,6 +1113,78 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     record_build(next, true, next_indices, itype, table_stride, index_base, batch, 1);
     next->prepared = true;
     next->dev.has_map = 1;
+    return DLRM_OK;
+}
+
+// ---- diagnostics: a native backtrace on a fatal signal (SIGSEGV / SIGBUS / SIGABRT), written to
+// stderr before the previous handler runs (Python's faulthandler then prints the Python stack).
+static struct sigaction g_prev[3];
+static const int g_sigs[3] = {SIGSEGV, SIGBUS, SIGABRT};
+static void fatal_trace(int sig, siginfo_t* si, void* uc) {
+    static const char head[] = "\n[dlrm] fatal signal, native backtrace (innermost first):\n";
+    (void)!write(2, head, sizeof head - 1);
+    char line[96];
+    const int n0 = snprintf(line, sizeof line, "[dlrm] signal %d, fault address %p\n", sig, si ? si->si_addr : nullptr);
+    if (n0 > 0) (void)!write(2, line, (size_t)n0);
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, n, 2);
+    for (int k = 0; k < 3; ++k)
+        if (g_sigs[k] == sig) {
+            sigaction(sig, &g_prev[k], nullptr);
+            if (g_prev[k].sa_flags & SA_SIGINFO) {
+                if (g_prev[k].sa_sigaction) {
+                    g_prev[k].sa_sigaction(sig, si, uc);
+                    return;
+                }
+            } else if (g_prev[k].sa_handler != SIG_DFL && g_prev[k].sa_handler != SIG_IGN) {
+                g_prev[k].sa_handler(sig);
+                return;
+            }
+        }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+int dlrm_debug_fatal_trace(int on) {
+    if (on == 2) {  // report who owns the handlers now (dladdr of the installed function), then arm
+        for (int k = 0; k < 3; ++k) {
+            struct sigaction cur;
+            if (sigaction(g_sigs[k], nullptr, &cur) != 0) continue;
+            void* fn = (cur.sa_flags & SA_SIGINFO) ? (void*)cur.sa_sigaction : (void*)cur.sa_handler;
+            Dl_info di;
+            memset(&di, 0, sizeof di);
+            const bool named = fn && dladdr(fn, &di) != 0;
+            fprintf(stderr, "[dlrm] signal %d handler %p (%s in %s)\n", g_sigs[k], fn,
+                    named && di.dli_sname ? di.dli_sname : "?", named && di.dli_fname ? di.dli_fname : "?");
+        }
+        fflush(stderr);
+    }
+    if (on) {  // an alternate signal stack for this thread: a stack overflow is a SIGSEGV too
+        static char* alt = nullptr;
+        if (!alt) alt = (char*)malloc(1 << 20);
+        if (alt) {
+            stack_t ss;
+            memset(&ss, 0, sizeof ss);
+            ss.ss_sp = alt;
+            ss.ss_size = 1 << 20;
+            (void)sigaltstack(&ss, nullptr);
+        }
+    }
+    for (int k = 0; k < 3; ++k) {
+        if (on) {
+            struct sigaction sa, old;
+            memset(&sa, 0, sizeof sa);
+            sa.sa_sigaction = fatal_trace;
+            sa.sa_flags = SA_SIGINFO | SA_RESETHAND | SA_ONSTACK;
+            sigemptyset(&sa.sa_mask);
+            if (sigaction(g_sigs[k], &sa, &old) != 0) return DLRM_E_ARG;
+            // (re-arming keeps the handler found the first time: chaining to ourselves would recurse)
+            if (!((old.sa_flags & SA_SIGINFO) && old.sa_sigaction == fatal_trace)) g_prev[k] = old;
+        } else {
+            sigaction(g_sigs[k], &g_prev[k], nullptr);
+        }
+    }
     return DLRM_OK;
 }
 

@@ -11,6 +11,8 @@
 #define WPH(k) do {} while (0)
 #endif
 
+#include "bitonic.hpp"
+
 namespace dlrm {
 
 constexpr int kChunk = 32;          // max positions of a segment handled by one lane group
@@ -911,6 +913,53 @@ struct SegPass {
     }
 };
 
+// ---- the part's sort in registers (round 6): n <= 256 keys (row >> vs, < 2^nbits) with their
+// index in the part's position-ordered list packed below them (IB = log2(64 R) bits), one
+// bitonic network (bitonic.hpp) over R = 1, 2 or 4 registers, then each sorted key written with
+// its position, read back through that index.  The same steps for any key distribution: skewed
+// rows cost what uniform ones do.  32-bit keys while nbits + IB <= 32, else 64-bit (the 292M-row
+// Terabyte table; its parts of more than 128 keys take the counting passes).
+template <int R, typename V>
+__device__ __forceinline__ void wave_sort_regs_r(int n, const uint32_t* K0, const int32_t* V0, uint32_t* K1,
+                                                 int32_t* V1) {
+    constexpr int IB = R == 1 ? 6 : (R == 2 ? 7 : (R == 4 ? 8 : 9));  // (n <= 64 R = 2^IB)
+    const int lane = threadIdx.x & 63;
+    V a[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * 64 + lane;
+        // (padding: all ones, above every real key -- a real key of all ones would need i = 2^IB - 1,
+        // i.e. n = 64 R, and then there is no padding)
+        a[r] = i < n ? (((V)K0[i] << IB) | (V)i) : ~(V)0;
+    }
+    wave_bitonic_sort<R>(a);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * 64 + lane;
+        if (i < n) {
+            K1[i] = (uint32_t)(a[r] >> IB);
+            V1[i] = V0[(int)(a[r] & (V)((1 << IB) - 1))];
+        }
+    }
+    wave_lds_sync();
+}
+
+constexpr int kRegSortMax = 256;  // largest part sorted in registers (else the counting passes)
+
+// Whether wave_sort_regs takes a part of n keys of nbits bits (uniform).
+__device__ __forceinline__ bool regsort_takes(int n, int nbits) {
+    return n > 1 && nbits > 0 && (n <= 128 || (n <= kRegSortMax && nbits + 8 <= 32));
+}
+
+// Sorts (K0, V0)[0, n) (LDS) into (K1, V1) by (key, position), where regsort_takes(n, nbits).
+__device__ __forceinline__ void wave_sort_regs(int n, int nbits, const uint32_t* K0, const int32_t* V0, uint32_t* K1,
+                                               int32_t* V1) {
+    if (n <= 64 && nbits + 6 <= 32) wave_sort_regs_r<1, uint32_t>(n, K0, V0, K1, V1);
+    else if (n <= 128 && nbits + 7 <= 32) wave_sort_regs_r<2, uint32_t>(n, K0, V0, K1, V1);
+    else if (n <= 128) wave_sort_regs_r<2, uint64_t>(n, K0, V0, K1, V1);
+    else wave_sort_regs_r<4, uint32_t>(n, K0, V0, K1, V1);
+}
+
 // The part the calling wave sorts and writes out: virtual table v = (t << vs) + part, its n keys
 // (row >> vs) and positions in position order at K0 / V0 (K1, V1, R: the same span of the pool's
 // other arrays, scratch).  Sorts them in LDS: keys wider than 8 bits by one unstable counting pass
@@ -921,7 +970,7 @@ struct SegPass {
 // order) and the once-hit flags; K0 / V0 hold the part's first (up to 8) keys / positions and R room
 // for one segment start -- the part is one segment, nothing is sorted.
 template <bool G, bool DIRECT = false>
-__device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
+__device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
                                int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, int g, int groups) {
     const int lane = threadIdx.x & 63;
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
@@ -931,6 +980,11 @@ __device__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint3
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
     if (DIRECT) {
+    } else if (!G && regsort_takes(n, nbits)) {  // (uniform: n, nbits)
+        WPH(3);
+        wave_sort_regs(n, nbits, K0, V0, K1, V1);
+        Ks = K1;
+        Vs = V1;
     } else if (n > 1 && nbits > 8 && wave_count_pass_unstable<G>(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
         WPH(3);
         wave_rank_buckets<G>(n, K1, V1, K0, V0, cnt);
@@ -1153,6 +1207,104 @@ __device__ __forceinline__ void wave_round_decode(WaveRound& o, const WaveRaw& r
     }
 }
 
+// ------------------------------------ wave build, N <= 2048, without the exchange (round 6, NOT used)
+// Measured slower and kept only as an A/B form (-DDLRM_WAVE_SCAN_SMALL): the standalone build's
+// loads ended at 2.2 us instead of 1.2 (each wave issues 4x the loads, lane-contiguous so every
+// load instruction touches 64 lines) and the branchy per-element placement took 2.6 us, against
+// 1.2 + 0.7 us for the exchange + barrier below; inside the apply launch the step's apply went
+// 11 -> 23.5 us (the build waves' extra VALU work beside the apply waves).
+// One build workgroup = parts q0 .. q0 + 3 of table t, one wave each, as below; but every wave
+// reads ALL of the table's N positions itself -- lane l the 4·E4 consecutive positions
+// [4·E4·l, 4·E4·(l + 1)), E4 = ceil(N / 256) 16-B loads (<= 8 KB per wave, from L2 after the
+// first) -- counts the workgroup's four parts (two DPP scans of 16-bit counters packed in pairs:
+// each lane's exclusive prefix per part, the wave's totals = the parts' sizes, hence the pool
+// regions), and appends only its OWN part's (key, position) pairs, in position order.  The four
+// waves exchange nothing: no workgroup barrier waits for the slowest wave's loads (round 5's
+// rounds form: counts + barrier 1.3 us, placement 0.9 us after the loads, p50).
+__device__ __forceinline__ void wave_build_group_small(const IndexerDev& ix, int g, int T,
+                                                       const TableDesc* __restrict__ tabs, const void* __restrict__ idx,
+                                                       int itype, int64_t tstride, int base, int N,
+                                                       unsigned* __restrict__ err, WaveBuildLds& sl) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
+    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
+    const uint32_t pmask = (1u << vs) - 1u;
+    constexpr uint32_t kBad = 0xffffffffu;  // (no row: nrows <= 2^32 - 1)
+    WPH(0);
+    constexpr int ME4 = kStepIndexMaxN / 256;
+    const int E4 = (N + 255) >> 8;
+    const int p0 = lane * 4 * E4;
+    const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
+    const bool vec = itype == DLRM_I32 && (N & 3) == 0 && ((uintptr_t)i32 & 15) == 0;
+    uint32_t xv[4 * ME4];  // row - base, or kBad (past N or out of range)
+    bool bad = false;
+    if (vec) {
+        int4 q[ME4];
+#pragma unroll
+        for (int j = 0; j < ME4; ++j) {
+            if (j < E4 && p0 + 4 * j < N) q[j] = ldg<int4>(i32 + p0 + 4 * j);
+            else q[j] = make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < ME4; ++j) {
+            const bool in = j < E4 && p0 + 4 * j < N;
+            const int e4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t x = (int64_t)e4[e] - base;
+                const bool ok = in && (uint64_t)x < (uint64_t)nrows;
+                bad |= in && !ok;
+                xv[4 * j + e] = ok ? (uint32_t)x : kBad;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4 * ME4; ++j) {
+            const bool in = j < 4 * E4 && p0 + j < N;
+            const int64_t x = load_index_if(in, idx, itype, (int64_t)t * tstride + p0 + j) - base;
+            const bool ok = in && (uint64_t)x < (uint64_t)nrows;
+            bad |= in && !ok;
+            xv[j] = ok ? (uint32_t)x : kBad;
+        }
+    }
+    WPH(7);
+    // out of range raises BoundsError; wave 0 of the workgroup of parts 0..3 reports it
+    if (q0 == 0 && w == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    // the workgroup's four parts: per lane counts, two 16-bit fields per word (<= 2048 per wave)
+    int c01 = 0, c23 = 0;
+#pragma unroll
+    for (int j = 0; j < 4 * ME4; ++j) {
+        const uint32_t q = xv[j] == kBad ? 4u : (xv[j] & pmask) - (uint32_t)q0;  // (>= 4: not this workgroup's)
+        c01 += q == 0u ? 1 : (q == 1u ? 0x10000 : 0);
+        c23 += q == 2u ? 1 : (q == 3u ? 0x10000 : 0);
+    }
+    const int i01 = wave_incl_scan(c01), i23 = wave_incl_scan(c23);
+    const int t01 = lane63(i01), t23 = lane63(i23);
+    const int n_of[kWaveParts] = {t01 & 0xffff, t01 >> 16, t23 & 0xffff, t23 >> 16};
+    int pb = 0;  // this wave's pool region: parts in order, 16-B aligned (wave_sort_part's vector reads)
+#pragma unroll
+    for (int q = 0; q < kWaveParts; ++q) pb += q < w ? (n_of[q] + 3) & ~3 : 0;
+    const int e01 = i01 - c01, e23 = i23 - c23;
+    int at = pb + (w == 0 ? e01 & 0xffff : w == 1 ? e01 >> 16 : w == 2 ? e23 & 0xffff : e23 >> 16);
+#pragma unroll
+    for (int j = 0; j < 4 * ME4; ++j) {
+        const uint32_t q = xv[j] == kBad ? 4u : (xv[j] & pmask) - (uint32_t)q0;
+        if (q == (uint32_t)w) {
+            sl.K[0][at] = xv[j] >> vs;
+            sl.V[0][at] = p0 + j;
+            ++at;
+        }
+    }
+    wave_lds_sync();
+    WPH(1);
+    const int n = n_of[w];
+    const int v = (t << vs) + q0 + w;
+    const int groups = (T << vs) / kWaveParts;
+    wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
+                          sl.cnt[w], g, groups);
+}
+
 // One build workgroup (kWaveParts waves = 256 threads): parts q0 .. q0 + 3 (q0 = 4 (g mod P / 4))
 // of table t = g / (P / 4), P = 2^vs >= 4 parts per table.  Every thread of the workgroup calls
 // it.  The four waves first split the table's positions among the four parts together -- in rounds
@@ -1170,6 +1322,12 @@ template <bool BIG = true>
 __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
                                  const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
                                  unsigned* __restrict__ err, WaveBuildLds& sl) {
+#ifdef DLRM_WAVE_SCAN_SMALL  // (tried, slower: every wave reading the whole table, see above)
+    if constexpr (!BIG) {
+        wave_build_group_small(ix, g, T, tabs, idx, itype, tstride, base, N, err, sl);
+        return;
+    }
+#endif
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
     const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;

@@ -87,6 +87,9 @@ class HotPath:
         self._prepare_ok = None  # build_split: None untried, False the wave build does not take it
         if self.pipeline:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
+            if self.pipeline == "apply" and self.B > 2048:  # (the in-apply wave build's parts, before any capture)
+                for ix in self._ixs:
+                    ix.reserve(self.B)
             self._ix_of = [None, None]  # the PackedIndices each indexer was last built from
             self._cur = 0
             self._pside = torch.cuda.Stream(device=dev)

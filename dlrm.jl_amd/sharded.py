@@ -125,6 +125,8 @@ class HipShardOps:
         self.lib = self.ctx.lib
         self.Bg, self.L, self.lr, self.base = batch_global, lookups, lr, index_base
         self.indexer = SparseIndexer(len(tables), batch_global * lookups, self.device) if tables else None
+        if self.indexer is not None and lookups == 1 and batch_global <= PREPARE_MAX_N:
+            self.indexer.reserve(batch_global)  # (the wave build's parts layout, before any capture)
         self.rts = self.ident = None
         self._prepare = None  # None: not tried yet; False: the wave build does not take this shape
 

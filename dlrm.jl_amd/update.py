@@ -129,6 +129,12 @@ class SparseIndexer:
         self._built_from = idx
         return True
 
+    def reserve(self, batch):
+        """Re-carves the indexer for wave builds of `batch` positions per table now (dlrm_indexer_reserve),
+        so that a graph capture with its first such build does not have to (the capture refuses it)."""
+        self.ctx.check(self.ctx.lib.dlrm_indexer_reserve(self.ctx.bind(), self.handle, int(batch)))
+        return self
+
     def nbytes(self):
         """Device bytes held (dlrm_indexer_bytes: grows on the first wave build of > 2048 positions)."""
         b = ctypes.c_int64()

@@ -82,6 +82,9 @@ int dlrm_ctx_create(int device, void* stream /* hipStream_t, NULL = default */, 
 int dlrm_ctx_destroy(dlrm_ctx* ctx);
 int dlrm_ctx_set_stream(dlrm_ctx* ctx, void* stream);
 const char* dlrm_last_error(const dlrm_ctx* ctx);
+/* Diagnostics: on = 1 installs handlers that print a native backtrace to stderr on SIGSEGV, SIGBUS
+ * or SIGABRT and then run the previous handler (0 restores them).  Not for production use. */
+int dlrm_debug_fatal_trace(int on);
 int dlrm_sync(dlrm_ctx* ctx);
 /* Synchronises, reads and clears the device out-of-range flag raised by any kernel since
  * the previous call.  DLRM_E_INDEX if it was set. */
@@ -260,6 +263,10 @@ int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables
  * parts -- ~112 B x 128 x 16384 = 235 MB per table at 16384 positions -- so run one such build
  * before graph capture (inside a capture it returns DLRM_E_ARG). */
 int dlrm_indexer_bytes(const dlrm_indexer* indexer, int64_t* bytes);
+/* Re-carves the indexer now for wave builds of `batch` positions per table (no-op when it already
+ * has that layout or batch <= 2048): call it before capturing a graph whose first wave build
+ * of > 2048 positions would otherwise re-carve it inside the capture. */
+int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* indexer, int batch);
 
 /* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
  * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only

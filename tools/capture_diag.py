@@ -6,7 +6,8 @@ before and after every host call, so the log shows whether the host blocks insid
 
     python tools/capture_diag.py OUTDIR variant[,variant...]
 
-variants: abi-eager, abi-op[:mode], torch-op[:mode], abi-step[:mode], torch-step[:mode], abi-step2, torch-step2
+variants: abi-eager, abi-op[:mode], torch-op[:mode], abi-step[:mode], torch-step[:mode], abi-step2, torch-step2,
+abi-step2m, torch-step2m, abi-step2raw[:mode], torch-step2raw[:mode] (raw HIP capture, graph inspected + dumped)
 (mode = torch.cuda.graph capture_error_mode: global (default) | thread_local | relaxed)
 """
 import faulthandler
@@ -96,11 +97,31 @@ def child(variant):
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
     ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
     micro = 2 if what == "step2" else 1
-    if what != "step2m":
+    if what not in ("step2m", "step2raw", "step2bigstack"):
         eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind, micro=micro)
         eng.step(x, idx, dout)
         torch.cuda.synchronize()
         mark("eager step ok")
+    if what == "step2raw":  # the M = 2 schedule that segfaulted, captured with raw HIP calls
+        raw_capture_m2(pkg, eng_args=(ops, TablePartition(T, 1), B, D, L, gpu, kind), x=x, idx=idx, dout=dout,
+                       mode=mode)
+        return
+    if what == "step2bigstack":  # the same in a thread with a 1 GiB stack (is it a stack overflow?)
+        import threading
+        threading.stack_size(1 << 30)
+        err = []
+
+        def body():
+            try:
+                raw_capture_m2(pkg, eng_args=(ops, TablePartition(T, 1), B, D, L, gpu, kind), x=x, idx=idx,
+                               dout=dout, mode=mode)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        th = threading.Thread(target=body)
+        th.start()
+        th.join()
+        mark(f"big-stack thread done: {err}")
+        return
     if what == "step2m":  # M = 2 schedule written out, a marker after every host call
         eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind, micro=2)
         eng.step(x, idx, dout)
@@ -181,6 +202,99 @@ def child(variant):
     mark("replay launched")
     torch.cuda.synchronize()
     mark("replay synced")
+
+
+NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "child-graph", 5: "empty", 6: "wait-event",
+              7: "event-record", 8: "ext-sem-signal", 9: "ext-sem-wait", 10: "mem-alloc", 11: "mem-free",
+              12: "memcpy-from-symbol", 13: "memcpy-to-symbol"}
+
+
+def raw_capture_m2(pkg, eng_args, x, idx, dout, mode):
+    """the M = 2 step with both exchanges on the SECOND (comm) stream, captured with
+    hipStreamBeginCapture / hipStreamEndCapture through ctypes instead of torch.cuda.graph, so the
+    captured graph can be inspected before it is instantiated: its node types, the nodes with no
+    dependency (roots) and no dependent (leaves), which stream each exchange's nodes joined from,
+    and a Graphviz dump (hipGraphDebugDotPrint).  Then hipGraphInstantiate, with the library's
+    native fatal-signal backtrace armed (dlrm_debug_fatal_trace), so a crash names its frame."""
+    import ctypes
+    import torch
+    from dlrm_jl_amd.sharded import ShardedHotPath
+    ops, part, B, D, L, gpu, kind = eng_args
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    lib = pkg._lib.load()
+    lib.dlrm_debug_fatal_trace(1)
+    mark("native fatal-signal backtrace armed")
+    eng = ShardedHotPath(ops, part, 0, B, D, L, torch.float32, gpu, exchange=kind, micro=2)
+    eng.step(x, idx, dout)
+    torch.cuda.synchronize()
+    mark("eager M=2 step ok")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    cmode = {"global": 0, "thread_local": 1, "relaxed": 2}[mode]
+    graph = vp()
+    with torch.cuda.stream(s):
+        main, cs = torch.cuda.current_stream(), eng._cstream
+        rc = hip.hipStreamBeginCapture(vp(main.cuda_stream), ctypes.c_int(cmode))
+        mark(f"hipStreamBeginCapture rc={rc}")
+        ev_look, ev_recv, ev_bwd, _ = eng._ev
+        for m in range(2):
+            eng.seg_lookup(idx, m)
+            ev_look[m].record(main)
+            cs.wait_event(ev_look[m])
+            with torch.cuda.stream(cs):
+                eng.exchange_fwd(m)
+                ev_recv[m].record(cs)
+        mark("forward exchanges recorded on the comm stream")
+        for m in range(2):
+            main.wait_event(ev_recv[m])
+            eng.seg_interact(x, dout, m)
+            ev_bwd[m].record(main)
+            cs.wait_event(ev_bwd[m])
+            with torch.cuda.stream(cs):
+                eng.exchange_bwd(m)
+        mark("backward exchanges recorded on the comm stream")
+        main.wait_stream(cs)
+        eng.seg_update(idx)
+        st = ctypes.c_int(-1)
+        hip.hipStreamIsCapturing(vp(cs.cuda_stream), ctypes.byref(st))
+        mark(f"comm stream capture status before end: {st.value} (1 = active)")
+        lib.dlrm_debug_fatal_trace(2)  # (re-armed last: RCCL / the runtime may have replaced it)
+        mark("handlers re-armed; hipStreamEndCapture ...")
+        rc = hip.hipStreamEndCapture(vp(main.cuda_stream), ctypes.byref(graph))
+        mark(f"hipStreamEndCapture rc={rc} graph={graph.value}")
+    n = ctypes.c_size_t(0)
+    hip.hipGraphGetNodes(graph, None, ctypes.byref(n))
+    nodes = (vp * n.value)()
+    hip.hipGraphGetNodes(graph, nodes, ctypes.byref(n))
+    hist, roots, leaves = {}, 0, 0
+    for i in range(n.value):
+        t = ctypes.c_int(-1)
+        hip.hipGraphNodeGetType(vp(nodes[i]), ctypes.byref(t))
+        name = NODE_TYPES.get(t.value, f"type{t.value}")
+        hist[name] = hist.get(name, 0) + 1
+        nd = ctypes.c_size_t(0)
+        hip.hipGraphNodeGetDependencies(vp(nodes[i]), None, ctypes.byref(nd))
+        ndp = ctypes.c_size_t(0)
+        hip.hipGraphNodeGetDependentNodes(vp(nodes[i]), None, ctypes.byref(ndp))
+        roots += nd.value == 0
+        leaves += ndp.value == 0
+    mark(f"captured graph: {n.value} nodes {hist}; roots {roots}, leaves {leaves}")
+    out = os.environ.get("DIAG_DOT", "/tmp/m2_graph.dot")
+    rc = hip.hipGraphDebugDotPrint(graph, out.encode(), ctypes.c_uint(0xffff))
+    mark(f"hipGraphDebugDotPrint rc={rc} -> {out}")
+    ex = vp()
+    mark("hipGraphInstantiate ...")
+    rc = hip.hipGraphInstantiate(ctypes.byref(ex), graph, None, None, ctypes.c_size_t(0))
+    mark(f"hipGraphInstantiate rc={rc}")
+    if rc == 0:
+        rc = hip.hipGraphLaunch(ex, vp(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        mark(f"replay rc={rc} synced")
+        hip.hipGraphExecDestroy(ex)
+    hip.hipGraphDestroy(graph)
+    eng.close()
+    mark("closed")
 
 
 def proc_state(pid):

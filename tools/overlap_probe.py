@@ -90,6 +90,12 @@ def par_loose(main, side):  # the side branch joins one step later
         main.wait_stream(side)
 
 
+want = sys.argv[1].split(",") if len(sys.argv) > 1 else None  # e.g. "parallel" (rocprofv3 timelines)
 for name, body in [("fwd", only_fwd), ("indexer", only_ix), ("seq", seq), ("parallel", par),
                    ("fwd x2 + side indexer", par_loose)]:
+    if want and name.split()[0] not in want:
+        continue
     print(f"{name:28s} {time_graph(body):8.2f} us/iter", flush=True)
+    torch.cuda.synchronize()
+    import time as _t
+    _t.sleep(0.05)  # (a gap in a kernel trace between the configurations)
