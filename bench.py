@@ -48,9 +48,9 @@ def parse():
                          "weak scaling, the workload's batch per GPU")
     ap.add_argument("--micro", type=int, default=0,
                     help="multi-GPU: micro-batches per step (the exchange of one overlaps the compute of the next); "
-                         "0: 1 -- with the whole step in one graph, a replay runs its parallel branches largely in "
-                         "series on this stack, so 2 measured 167 us against 157 us (tools/shard_sim.py, world 8, "
-                         "stand-in exchanges; DESIGN.md §6)")
+                         "0: 1 -- M = 2 halves every launch and its exchanges must stay on the capture's origin "
+                         "stream (RCCL captured on a forked stream crashes hipStreamEndCapture on this HIP), so it "
+                         "measured 161 us against 160 us (tools/shard_sim.py, world 8, stand-in exchanges; DESIGN.md §6)")
     ap.add_argument("--shard-graph", choices=["full", "segments"], default="full",
                     help="multi-GPU graph form: 'full' (default) = one hipGraph per step with the RCCL "
                          "all-to-alls inside (falls back to 'segments' where the capture is refused, e.g. gloo); "

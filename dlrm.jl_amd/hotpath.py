@@ -79,7 +79,8 @@ class HotPath:
         #   "apply" (`step_prep`): by extra workgroups of this step's apply launch
         #           (dlrm_step_bwd_prepare) -- the indexer's latency hides behind the apply's;
         #   "side"  (`step_next`): by its own launch on a side stream (measured slower: a replayed
-        #           hipGraph runs the side branch serially).
+        #           hipGraph runs the branch concurrently, but it slows the kernels beside it and each
+        #           step pays two cross-queue hops of ~3.7 us: DESIGN.md §6).
         mode = {False: None, 0: None, None: None, True: "side", 1: "side", 2: "apply"}.get(pipeline, pipeline)
         if mode not in (None, "side", "apply"):
             raise ValueError(f"pipeline must be None, 'side' or 'apply', not {pipeline!r}")

@@ -352,6 +352,17 @@ mutable struct HipIndexer
     end
 end
 
+"Re-carves the indexer for wave builds of `batch` positions per table now (before capturing a graph)."
+reserve!(ix::HipIndexer, batch::Integer) =
+    check(ix.ctx, ccall((:dlrm_indexer_reserve, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), ix.ctx.ptr, ix.ptr, batch))
+"Device bytes the indexer holds."
+function nbytes(ix::HipIndexer)
+    b = Ref{Int64}(0)
+    rc = ccall((:dlrm_indexer_bytes, libdlrm), Cint, (Ptr{Cvoid}, Ref{Int64}), ix.ptr, b)
+    rc == 0 || throw(DLRMError(rc, "dlrm_indexer_bytes"))
+    return Int(b[])
+end
+
 const INDEXERS = IdDict{Any,HipIndexer}()
 
 # `num_splits` / `nthreads` tune the CPU scatter; the GPU kernel has its own decomposition.

@@ -97,7 +97,7 @@ def child(variant):
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32) * 1e-2).to(gpu)
     ops = HipShardOps([torch.from_numpy(t).to(gpu) for t in tabs], B, L, 0.25, device=gpu)
     micro = 2 if what == "step2" else 1
-    if what not in ("step2m", "step2raw", "step2bigstack"):
+    if what not in ("step2m", "step2raw", "step2bigstack", "step2fresh"):
         eng = ShardedHotPath(ops, TablePartition(T, 1), 0, B, D, L, torch.float32, gpu, exchange=kind, micro=micro)
         eng.step(x, idx, dout)
         torch.cuda.synchronize()
@@ -105,6 +105,10 @@ def child(variant):
     if what == "step2raw":  # the M = 2 schedule that segfaulted, captured with raw HIP calls
         raw_capture_m2(pkg, eng_args=(ops, TablePartition(T, 1), B, D, L, gpu, kind), x=x, idx=idx, dout=dout,
                        mode=mode)
+        return
+    if what == "step2fresh":  # exchanges on the second stream(s), one fresh stream per exchange
+        raw_capture_m2(pkg, eng_args=(ops, TablePartition(T, 1), B, D, L, gpu, kind), x=x, idx=idx, dout=dout,
+                       mode=mode, fresh=True)
         return
     if what == "step2bigstack":  # the same in a thread with a 1 GiB stack (is it a stack overflow?)
         import threading
@@ -209,7 +213,7 @@ NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "child-graph"
               12: "memcpy-from-symbol", 13: "memcpy-to-symbol"}
 
 
-def raw_capture_m2(pkg, eng_args, x, idx, dout, mode):
+def raw_capture_m2(pkg, eng_args, x, idx, dout, mode, fresh=False):
     """the M = 2 step with both exchanges on the SECOND (comm) stream, captured with
     hipStreamBeginCapture / hipStreamEndCapture through ctypes instead of torch.cuda.graph, so the
     captured graph can be inspected before it is instantiated: its node types, the nodes with no
@@ -238,23 +242,32 @@ def raw_capture_m2(pkg, eng_args, x, idx, dout, mode):
         rc = hip.hipStreamBeginCapture(vp(main.cuda_stream), ctypes.c_int(cmode))
         mark(f"hipStreamBeginCapture rc={rc}")
         ev_look, ev_recv, ev_bwd, _ = eng._ev
+        # fresh: every exchange on a stream of its own, forked from the origin stream once and joined
+        # once (no stream both waits on the origin and is waited on by it more than one time)
+        xs = [torch.cuda.Stream() for _ in range(4)] if fresh else [cs] * 4
+        ev_done = [torch.cuda.Event() for _ in range(4)]
         for m in range(2):
             eng.seg_lookup(idx, m)
             ev_look[m].record(main)
-            cs.wait_event(ev_look[m])
-            with torch.cuda.stream(cs):
+            xs[m].wait_event(ev_look[m])
+            with torch.cuda.stream(xs[m]):
                 eng.exchange_fwd(m)
-                ev_recv[m].record(cs)
-        mark("forward exchanges recorded on the comm stream")
+                ev_recv[m].record(xs[m])
+        mark("forward exchanges recorded on the comm stream(s)")
         for m in range(2):
             main.wait_event(ev_recv[m])
             eng.seg_interact(x, dout, m)
             ev_bwd[m].record(main)
-            cs.wait_event(ev_bwd[m])
-            with torch.cuda.stream(cs):
+            xs[2 + m].wait_event(ev_bwd[m])
+            with torch.cuda.stream(xs[2 + m]):
                 eng.exchange_bwd(m)
-        mark("backward exchanges recorded on the comm stream")
-        main.wait_stream(cs)
+                ev_done[2 + m].record(xs[2 + m])
+        mark("backward exchanges recorded on the comm stream(s)")
+        if fresh:
+            for m in range(2):
+                main.wait_event(ev_done[2 + m])
+        else:
+            main.wait_stream(cs)
         eng.seg_update(idx)
         st = ctypes.c_int(-1)
         hip.hipStreamIsCapturing(vp(cs.cuda_stream), ctypes.byref(st))
