@@ -63,6 +63,9 @@ def parse():
                          "2.10M vs 2.00M samples/s: eager lets the side-stream indexer overlap the gather)")
     ap.add_argument("--overlap-indexer", type=int, default=-1, help="-1: the engine's default")
     ap.add_argument("--fused", type=int, default=1)
+    ap.add_argument("--chunk", type=int, default=-1,
+                    help="the wave build's chunk limit (16 or 32; 0: the library's default 32); -1 (default): "
+                         "pkg.step_chunk (16 for uniform one-hot batches, 32 for Zipf rows)")
     ap.add_argument("--materialize-ys", type=int, default=-1,
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
                          "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
@@ -391,7 +394,8 @@ def main():
                              overlap_indexer=None if a.overlap_indexer < 0 else bool(a.overlap_indexer),
                              fused=bool(a.fused),
                              materialize_ys=None if a.materialize_ys < 0 else bool(a.materialize_ys),
-                             pipeline={0: None, 1: "side", 2: "apply"}[a.pipeline])
+                             pipeline={0: None, 1: "side", 2: "apply"}[a.pipeline],
+                             chunk=pkg.step_chunk(w) if a.chunk < 0 else (a.chunk or None))
         F = T + 1
         dtp = tables[0].dtype
         x = torch.randn((B, D), device=dev, generator=g).to(dtp)
@@ -641,6 +645,9 @@ def main():
         bytes_ = algorithmic_bytes(w, B, T, D, L, E, 4, uniq, chunks, engine.materialize_ys)
         # one prebuilt indexer per index batch, so the update stage can be timed on its own
         indexers = [pkg.SparseIndexer(T, B * L, dev) for _ in range(nb)]  # not the engine's own
+        for ix in indexers:
+            if engine.chunk:
+                ix.set_chunk(engine.chunk)  # (the engine's chunk limit)
         home = engine.indexer
         for k in range(nb):
             engine.indexer = indexers[k]
@@ -676,6 +683,9 @@ def main():
         if engine.pipeline == "apply":  # the next batch's indexer built by the apply launch
             names = ["lookup_interact_fwd", "interact_bwd", "sgd_update"]
             nxt = [pkg.SparseIndexer(T, B * L, dev) for _ in range(2)]
+            for ix in nxt:
+                if engine.chunk:
+                    ix.set_chunk(engine.chunk)
 
             def apply_prep_k(k):
                 engine.indexer = indexers[k]
@@ -821,6 +831,7 @@ def main():
                                        + ("RCCL all-to-all" if dist.get_backend() == "nccl" else
                                           f"{dist.get_backend()} all-to-all (host-staged rehearsal)")),
                        "index_batches": nb,
+                       **({"chunk_limit": engine.chunk or 32} if world == 1 and engine.step_api else {}),
                        **({"micro_batches": engine.M} if world > 1 else {}),
                        "launch": (f"hipGraph replay (<= {chunk} steps per graph)" if graphs is not None else
                                   "hipGraph replay of each whole step, RCCL all-to-alls captured inside"

@@ -699,6 +699,7 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->dev.cap = cap;
     ix->dev.pcap = indexer_slice_cap(cap);
     ix->dev.pdim = kPartialDim;
+    ix->dev.chunk_max = kChunk;
     const int64_t hs = cap > kFastMaxN ? hix_table_slots(cap) : 0;
     ix->dev.hsize = hs;
     ix->dev.hbits = 0;
@@ -712,6 +713,13 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
         return rc;
     }
     *out = ix;
+    return DLRM_OK;
+}
+
+int dlrm_indexer_set_chunk(dlrm_ctx* ctx, dlrm_indexer* ix, int max_positions) {
+    CHECK_ARG(ctx && ix, "dlrm_indexer_set_chunk: null argument");
+    CHECK_ARG(max_positions == 16 || max_positions == 32, "dlrm_indexer_set_chunk: %d (16 or 32)", max_positions);
+    ix->dev.chunk_max = max_positions;
     return DLRM_OK;
 }
 

@@ -304,6 +304,7 @@ struct IndexerDev {
     // this indexer folds it into the ctx's flag (its lookups raise the same errors; this covers a
     // prebuilt update without one)
     const unsigned* build_err;
+    int chunk_max;         // the wave build's chunk limit (16 or 32; indexer.hpp kMinChunk .. kChunk)
     int has_map;
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)

@@ -15,7 +15,15 @@
 
 namespace dlrm {
 
-constexpr int kChunk = 32;          // max positions of a segment handled by one lane group
+#ifndef DLRM_CHUNK
+#define DLRM_CHUNK 32
+#endif
+constexpr int kChunk = DLRM_CHUNK;  // max positions of a segment handled by one lane group
+// The wave build's chunk limit is chosen per indexer at run time (IndexerDev::chunk_max: 16 or 32,
+// dlrm_indexer_set_chunk; round 6): at 16, segments of 17..32 positions become one-slice hot
+// items, run by a whole workgroup in one round of grad loads instead of two rounds by one lane
+// group.  kMinChunk bounds the slice counts the allocations are sized for.
+constexpr int kMinChunk = 16;
 constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
 enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
 // Hot segments are cut into slices of kHotSlice positions, one work item (one 256-thread apply
@@ -855,8 +863,8 @@ struct SegPass {
         const int beg = ok ? R[s] : 0;
         const int end = ok ? (s + 1 < U ? R[s + 1] : n) : 0;
         const int len = end - beg;
-        const bool isc = ok && len >= 2 && len <= kChunk;
-        const bool ish = ok && len > kChunk;
+        const bool isc = ok && len >= 2 && len <= ix.chunk_max;
+        const bool ish = ok && len > ix.chunk_max;
         const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
         const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
         const int sincl = wave_incl_scan(ns);
@@ -1005,9 +1013,10 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     // One pass over the sorted keys, four consecutive keys per lane (16-B LDS reads: the part's
     // region starts 16-B aligned): perm and the once-hit flags stored, segment starts R[s], and the
     // counts that size the wave's share of the flat lists -- chunks (a head that is not a tail and
-    // whose key differs kChunk places on: 2 .. kChunk positions) and hot segments (longer), whose
+    // whose key differs cm places on: 2 .. cm positions) and hot segments (longer), whose
     // slices are counted from R after.  (Its stores precede the reservation atomic below; they
     // complete before it returns anyway.)
+    const int cm = ix.chunk_max;  // this build's chunk limit (16 or 32)
     const int64_t off = (int64_t)v * ix.cap;
     int32_t* perm = ix.perm + off;
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
@@ -1015,15 +1024,15 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     int U = 0, C = 0, H = 0;
     if (DIRECT) {
         U = n > 0 ? 1 : 0;
-        C = n >= 2 && n <= kChunk ? 1 : 0;
-        H = n > kChunk ? 1 : 0;
+        C = n >= 2 && n <= cm ? 1 : 0;
+        H = n > cm ? 1 : 0;
         if (lane == 0) R[0] = 0;
     }
     for (int j0 = 0; j0 < (DIRECT ? 0 : n); j0 += 256) {
         const int i = j0 + 4 * lane;
         const uint4 k4 = *(const uint4*)(Ks + i);  // (past n: garbage, masked below)
         const int4 v4 = *(const int4*)(Vs + i);
-        const uint4 kf = *(const uint4*)(Ks + i + kChunk);
+        const uint4 kf = *(const uint4*)(Ks + i + cm);  // (cm % 4 == 0: 16-B aligned)
         const uint32_t kp = Ks[i > 0 ? i - 1 : 0], kn = Ks[i + 4];
         const uint32_t kk[6] = {kp, k4.x, k4.y, k4.z, k4.w, kn};
         const uint32_t kfa[4] = {kf.x, kf.y, kf.z, kf.w};
@@ -1036,7 +1045,7 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
             const bool ok = ie < n;
             const bool head = ok && (ie == 0 || kk[e] != kk[e + 1]);
             const bool tail = ok && (ie + 1 == n || kk[e + 2] != kk[e + 1]);
-            const bool longer = ok && ie + kChunk < n && kfa[e] == kk[e + 1];
+            const bool longer = ok && ie + cm < n && kfa[e] == kk[e + 1];
             hd[e] = head;
             nh += head ? 1 : 0;
             nc += (head && !tail && !longer) ? 1 : 0;
@@ -1062,11 +1071,11 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     }
     part_sync<G>();
     int S = 0;
-    if (H)  // (rows hit more than kChunk times in this part: small tables)
+    if (H)  // (rows hit more than cm times in this part: small tables)
         for (int s0 = 0; s0 < U; s0 += 64) {
             const int s = s0 + lane;
             const int len = s < U ? (s + 1 < U ? R[s + 1] : n) - R[s] : 0;
-            S += lane63(wave_incl_scan(len > kChunk ? (len + kHotSlice - 1) / kHotSlice : 0));
+            S += lane63(wave_incl_scan(len > cm ? (len + kHotSlice - 1) / kHotSlice : 0));
         }
     // The wave reserves its flat-list ranges and arrives in ONE atomic add (lane 0): the segment
     // stores below run while it is in flight, and only the flat records wait for it.

@@ -88,7 +88,7 @@ constexpr int kBuildWaves = kBuildThreads / 64;
 constexpr int kLdsSortMax = 2048;   // positions per table sorted entirely in LDS
 constexpr int kDigits = 257;        // 256 row digits + 1 bucket that keeps invalid indices last
 
-int64_t indexer_slice_cap(int64_t cap) { return cap / kHotSlice + cap / (kChunk + 1) + 1; }
+int64_t indexer_slice_cap(int64_t cap) { return cap / kHotSlice + cap / (kMinChunk + 1) + 1; }
 
 template <typename V>
 __device__ __forceinline__ V block_scan_excl(V v, V* wtot, V* tot) { return block_scan_nw<kBuildWaves, V>(v, wtot, tot); }
@@ -789,7 +789,7 @@ static void launch_apply_vec(hipStream_t s, const IndexerDev& ix, TableDesc* tab
     // persistent grid: resident workgroups only (never more than the worst-case item count per
     // table: N / kHotSlice + N / (kChunk + 1) + 1 hot slices, N / NG chunk items, singles items)
     const int64_t SP = G::NG * G::SPPG;
-    const int64_t ib = (int64_t)T_ * (N / kHotSlice + N / (kChunk + 1) + 1 + (N + G::NG - 1) / G::NG) +
+    const int64_t ib = (int64_t)T_ * (N / kHotSlice + N / (kMinChunk + 1) + 1 + (N + G::NG - 1) / G::NG) +
                        (sa.single ? (int64_t)(T_ >> ix.vshift) * ((N + SP - 1) / SP) : 0);
     static int per_cu = 0;
     if (!per_cu) {

@@ -37,7 +37,7 @@ from .update import SparseIndexer
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None, pipeline=False):
+                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None, pipeline=False, chunk=None):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -61,6 +61,10 @@ class HotPath:
         self.dx = torch.empty((self.B, self.d), dtype=torch.float32, device=dev)
         self.dt = torch.empty((self.B, self.F * self.d), dtype=torch.float32, device=dev)
         self.indexer = SparseIndexer(self.T, self.B * self.L, dev) if deterministic else None
+        # the wave build's chunk limit (None: the library's 32; shapes.step_chunk picks per workload)
+        self.chunk = chunk
+        if chunk is not None and self.indexer is not None:
+            self.indexer.set_chunk(chunk)
         self.ctx = self.ts.ctx
         self.lib = self.ctx.lib
         self.dcode = dtype_code(dt)
@@ -88,6 +92,8 @@ class HotPath:
         self._prepare_ok = None  # build_split: None untried, False the wave build does not take it
         if self.pipeline:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
+            if chunk is not None:
+                self._ixs[1].set_chunk(chunk)
             if self.pipeline == "apply" and self.B > 2048:  # (the in-apply wave build's parts, before any capture)
                 for ix in self._ixs:
                     ix.reserve(self.B)

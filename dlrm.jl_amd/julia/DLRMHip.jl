@@ -355,6 +355,10 @@ end
 "Re-carves the indexer for wave builds of `batch` positions per table now (before capturing a graph)."
 reserve!(ix::HipIndexer, batch::Integer) =
     check(ix.ctx, ccall((:dlrm_indexer_reserve, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), ix.ctx.ptr, ix.ptr, batch))
+"The wave build's chunk limit for the indexer's later builds (16 or 32; deterministic either way)."
+set_chunk!(ix::HipIndexer, max_positions::Integer) =
+    check(ix.ctx, ccall((:dlrm_indexer_set_chunk, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), ix.ctx.ptr, ix.ptr,
+                        max_positions))
 "Device bytes the indexer holds."
 function nbytes(ix::HipIndexer)
     b = Ref{Int64}(0)

@@ -66,6 +66,18 @@ def step_pipeline(w):
     return "apply" if B <= APPLY_MAX_N else "side"
 
 
+def step_chunk(w):
+    """The wave build's chunk limit for workload `w` (HotPath(chunk=...), dlrm_indexer_set_chunk):
+    16 for uniform one-hot batches -- the 105-row Kaggle table's 17..32-position segments then run
+    as one-round hot-slice items: metric step 36.9 -> 36.4 us, 55.5 -> 56.1 M samples/s in an
+    alternating A/B, D = 16 unchanged (profiles/r14/chunk16_ab_*) -- and 32 for Zipf rows, whose
+    many more such segments turn into more hot-slice items than the apply launch has workgroups
+    (Terabyte bf16 52.5 -> 51.8 M with 16)."""
+    if w["lookups"] != 1 or w.get("zipf"):
+        return None
+    return 16
+
+
 def table_bytes(rows, dim, esize):
     return sum(rows) * dim * esize
 

@@ -135,6 +135,11 @@ class SparseIndexer:
         self.ctx.check(self.ctx.lib.dlrm_indexer_reserve(self.ctx.bind(), self.handle, int(batch)))
         return self
 
+    def set_chunk(self, max_positions):
+        """The wave build's chunk limit for later builds (16 or 32; dlrm_indexer_set_chunk)."""
+        self.ctx.check(self.ctx.lib.dlrm_indexer_set_chunk(self.ctx.bind(), self.handle, int(max_positions)))
+        return self
+
     def nbytes(self):
         """Device bytes held (dlrm_indexer_bytes: grows on the first wave build of > 2048 positions)."""
         b = ctypes.c_int64()

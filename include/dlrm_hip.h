@@ -267,6 +267,12 @@ int dlrm_indexer_bytes(const dlrm_indexer* indexer, int64_t* bytes);
  * has that layout or batch <= 2048): call it before capturing a graph whose first wave build
  * of > 2048 positions would otherwise re-carve it inside the capture. */
 int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* indexer, int batch);
+/* The wave build's chunk limit for this indexer's later builds (16 or 32, default 32): segments of
+ * at most this many positions become chunk items (one lane group each), longer ones hot-slice items
+ * (a workgroup each).  16 turns the 17..32-position segments of uniform one-hot batches (the
+ * 105-row Kaggle table) into one-round items (DESIGN.md §3 "Round 6").  Deterministic either way; a
+ * 17..32-position segment is summed in a different (fixed) order, so its fp32 rounding may differ. */
+int dlrm_indexer_set_chunk(dlrm_ctx* ctx, dlrm_indexer* indexer, int max_positions);
 
 /* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
  * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only

@@ -153,8 +153,9 @@ def test_bench_form_vs_oracle(pkg, gpu, workload):
     rng = np.random.default_rng(B + D)
     batches = [np.stack([rng.integers(0, n, size=B) for n in w["rows"]]).astype(np.int64) for _ in range(2)]
     pipeline = pkg.step_pipeline(w)
-    hp = run_step_vs_oracle(pkg, gpu, tables, batches, B, 1, 0.05, dtype, seed=B, pipeline=pipeline)
-    assert hp.step_api
+    hp = run_step_vs_oracle(pkg, gpu, tables, batches, B, 1, 0.05, dtype, seed=B, pipeline=pipeline,
+                            hot_kw={"chunk": pkg.step_chunk(w)})
+    assert hp.step_api and hp.chunk == pkg.step_chunk(w)
 
 
 # ---------------------------------------------------------------------------- configs[2]
