@@ -83,7 +83,8 @@ const Knobs& knobs() {
                          env_int("DLRM_RELU_2PASS", 1) == 0, env_int("DLRM_BWD_YS", 1) == 0,
                          env_int("DLRM_BWD_SPLIT", 1) == 0,  env_int("DLRM_BWD_SPB", 0),
                          env_int("DLRM_BWD_CPL", 0),         env_int("DLRM_UPD_SBU", 1),
-                         env_int("DLRM_WAVE_ROUNDS", 0)};
+                         env_int("DLRM_WAVE_ROUNDS", 0),     env_int("DLRM_BAG_WAVE", 1) == 0,
+                         env_int("DLRM_BAG_VS", 0)};
     return k;
 }
 int ctx_device(dlrm_ctx* ctx) { return ctx->device; }
@@ -116,7 +117,7 @@ static int hip_set(dlrm_ctx* ctx) { return ctx_hip(ctx, hipSetDevice(ctx->device
 static int step_parts_log2(int dflt = kStepParts) {
     const int forced = knobs().step_parts;
     const int p = forced > 0 ? forced : dflt;
-    return p >= 16 ? 4 : (p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0)));
+    return p >= 32 ? 5 : (p >= 16 ? 4 : (p >= 8 ? 3 : (p >= 4 ? 2 : (p >= 2 ? 1 : 0))));
 }
 
 // vshift of the wave build of `batch` positions per table (the step forward's in-launch build and
@@ -588,36 +589,41 @@ int dlrm_interact_bwd_blocked(dlrm_ctx* ctx, const dlrm_tables* tb, const void* 
 
 // --------------------------------------------------------------------------- indexer
 // Footprint.  The per-part arrays (perm, seg_start, seg_row, chunks, hot, hot_slice, hot_cnt: 92 B
-// per slot; + 20 B of HBM sort scratch above 2048 positions) hold `parts` virtual tables of cap
-// slots per table, because one part may receive every position of its table (a hot row).  An
-// indexer is created with the parts the builds up to 2048 positions use (16 per table, or fewer
-// for a smaller cap); a wave build of more positions (dlrm_indexer_prepare, dlrm_step_bwd_prepare:
-// 2^wave_vshift(N) parts, 128 at 16384) re-carves it with that many on first use -- outside graph
-// capture (26 tables at cap 16384 were ~7 GB per indexer from creation on, whether or
-// not a wave build ever ran).  Partial rows of multi-slice hot segments are per real table (the
-// wave build's item map indexes them by its flat slice number, at most pcap per table), times
-// the <= 8 parts of the builds without an item map.
+// per slot; + 20 B of HBM sort scratch above 2048 positions) are cap slots per table: the wave
+// builds pack a table's parts back to back (common.hpp kSegPad, "compact" layout), whatever the
+// parts (256 per table at 32768 positions).  Only the in-LDS parts build of 4096 < N <= 8192
+// (fast_index_table, 8 parts, v * cap) needs 8 virtual tables of cap slots per table, so an
+// indexer whose cap is in that range is carved with 8.  (Round 5 gave every wave-build part a whole
+// cap and re-carved on first use: 128 x the table at 16384 positions, ~7 GB per indexer for 26
+// tables)  Partial rows of multi-slice hot segments are per real table (the wave
+// build's item map indexes them by its flat slice number, at most pcap per table), times the <= 8
+// parts of the builds without an item map.
 static int64_t partial_rows(const dlrm_indexer* ix) {
     const int64_t T0 = ix->T > 0 ? ix->T : 1;
     const int64_t cap = ix->dev.cap;
-    const int np = cap <= kPartsMaxN ? (indexer_parts(cap) < 8 ? indexer_parts(cap) : 8) : 1;
+    const int np = cap <= kPartsMaxN ? 8 : 1;
     return T0 * np * ix->dev.pcap;
 }
 
-// (Re)carves every array of the indexer for `parts` virtual tables per table (contents reset).
+// Carves every array of the indexer for `parts` virtual tables per table (contents reset).
 static int indexer_carve(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
     const int64_t cap = ix->dev.cap;
     const int64_t T0 = ix->T > 0 ? ix->T : 1;
     const int64_t T = (int64_t)parts * T0;
     const int64_t hs = ix->dev.hsize;
+    // the largest wave build this indexer takes: 2^vw parts per table, T0 << vw / 4 workgroups (>= 32
+    // parts: the builds of <= 2048 positions may take 32, DLRM_STEP_PARTS)
+    const int vw = std::max(wave_vshift(cap < kWaveMaxN ? cap : kWaveMaxN), 5);
+    const int64_t TW = T0 << vw;
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
-    const size_t n = (size_t)(T * cap), n1 = (size_t)(T * (cap + 1)), n0 = (size_t)(T0 * cap);
-    // the wave build's flat item lists: kResLists sub-lists of res_stride records (indexer.hpp), for
-    // the largest build this layout takes (T / 4 workgroups); the HBM sort scratch for cap > 2048
-    const size_t nrec = T >= 4 ? (size_t)kResLists * (size_t)res_stride((int)(T / 4), cap) + 64 : 64;
-    // (only the wave builds of > 2048 positions, which have > 16 parts, can sort in HBM)
-    const int64_t wstride = cap > kStepIndexMaxN && parts > (1 << 4) ? T * cap + 64 : 0;
+    const size_t n = (size_t)(T * cap), n0 = (size_t)(T0 * cap);
+    const size_t n1 = (size_t)std::max(T * (cap + 1), T0 * (cap + kSegPad));  // (compact: a sentinel per part)
+    const size_t ncnt = (size_t)std::max(T, TW);
+    // the wave build's flat item lists: kResLists sub-lists of res_stride records (indexer.hpp); the
+    // HBM sort scratch (5 arrays, compact) for the builds of more than 2048 positions
+    const size_t nrec = (size_t)kResLists * (size_t)res_stride((int)(TW / 4), cap, vw) + 64;
+    const int64_t wstride = cap > kStepIndexMaxN ? T0 * cap + 64 : 0;
     IndexerDev d = ix->dev;
     float* partial_keep = ix->partial_big ? d.partial : nullptr;  // (a grown partial buffer stays)
     Piece pieces[] = {
@@ -626,7 +632,7 @@ static int indexer_carve(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
         {(void**)&d.seg_row, n * 4},   {(void**)&d.chunks, n * 32}, {(void**)&d.hot, n * 16},
         {(void**)&d.hot_slice, n * 16}, {(void**)&d.hot_cnt, n * 4},
         {(void**)&d.partial, partial_keep ? 0 : (size_t)partial_rows(ix) * kPartialDim * 4},
-        {(void**)&d.counts, (size_t)T * 32},   {(void**)&d.single, n0},
+        {(void**)&d.counts, ncnt * 32},   {(void**)&d.single, n0},
         {(void**)&ix->prep_err, 16},
         {(void**)&d.slice_rec, nrec * 32}, {(void**)&d.chunk_rec, nrec * 32},
         {(void**)&d.wscratch, (size_t)wstride * 5 * 4},
@@ -670,20 +676,10 @@ static int indexer_carve(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
     return DLRM_OK;
 }
 
-// The parts layout a wave build of `vs` (> 4: more than 2048 positions per table) needs, re-carved
-// on first use.  Refused while the ctx's stream is being captured (hipFree would break the capture):
-// run one step of that shape before capturing.
-static int ensure_parts(dlrm_ctx* ctx, dlrm_indexer* ix, int vs) {
-    if (has_parts(ix, vs)) return DLRM_OK;
-    if ((1 << vs) > indexer_parts(ix->dev.cap))
-        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "indexer of %lld positions per table: no %d-part layout",
-                        (long long)ix->dev.cap, 1 << vs);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(ctx->stream, &cs);
-    if (cs != hipStreamCaptureStatusNone)
-        return ctx_fail(ctx, DLRM_E_ARG, "the first wave build of > %d positions per table re-carves the indexer "
-                        "(%d parts per table): run it once before graph capture", kStepIndexMaxN, 1 << vs);
-    return indexer_carve(ctx, ix, 1 << vs);
+// Whether a wave build of `batch` positions per table fits this indexer (compact layout: any parts;
+// the flat records hold global perm entries in int32).
+static bool wave_fits(const dlrm_indexer* ix, int64_t batch) {
+    return batch <= ix->dev.cap && batch <= kWaveMaxN && (int64_t)(ix->T > 0 ? ix->T : 1) * ix->dev.cap < (1ll << 31);
 }
 
 int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm_indexer** out) {
@@ -704,9 +700,9 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups, dlrm
     ix->dev.hsize = hs;
     ix->dev.hbits = 0;
     while (((int64_t)1 << ix->dev.hbits) < hs) ++ix->dev.hbits;
-    // the parts of the builds up to 2048 positions per table (16, or fewer for a smaller cap); the
-    // larger wave builds re-carve with more (ensure_parts)
-    const int parts = indexer_parts(cap) < (1 << 4) ? indexer_parts(cap) : (1 << 4);
+    // 8 virtual tables per table for the in-LDS parts build of kFastMaxN < N <= kPartsMaxN (fast_index_table;
+    // build_vshift <= 3), else one: every wave build packs its parts per table
+    const int parts = cap > kFastMaxN && cap <= kPartsMaxN ? (1 << 3) : 1;
     const int rc = indexer_carve(ctx, ix, parts);
     if (rc != DLRM_OK) {
         delete ix;
@@ -727,8 +723,8 @@ int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* ix, int batch) {
     CHECK_ARG(ctx && ix, "dlrm_indexer_reserve: null argument");
     CHECK_ARG(batch >= 0 && batch <= ix->dev.cap, "dlrm_indexer_reserve: batch %d > capacity %lld", batch,
               (long long)ix->dev.cap);
-    if (batch <= kStepIndexMaxN || batch > kWaveMaxN || ix->T == 0) return DLRM_OK;  // (nothing to re-carve)
-    return ensure_parts(ctx, ix, wave_parts_log2(batch));
+    // (round 6: the wave builds' compact layout needs no re-carving; nothing to do)
+    return DLRM_OK;
 }
 
 int dlrm_indexer_bytes(const dlrm_indexer* ix, int64_t* bytes) {
@@ -764,6 +760,23 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
     // listed as one-position chunks; the apply then updates them with no descriptor read
     const int64_t N = (int64_t)batch * lookups;
     const bool split = N <= kFastMaxN || (ix->dev.hsize && N <= kHixMaxN);
+    if (split && N > kPartsMaxN && wave_fits(ix, N) && !knobs().bag_hash) {
+        // pooled bags (configs[4]: 20480 positions per table) and other large batches: the bag build
+        // (update.hip: count, place by part, then the wave build's per-part sort; 2^wave_vshift(N)
+        // parts per table, flat item map) instead of the hash build (4 launches, global atomics;
+        // round 5: 146 us and 13x its algorithmic bytes for configs[4]).  It groups positions
+        // p = b L + k; the apply maps p to its bag.  Bounds errors go to the ctx's flag, as every
+        // dlrm_indexer_build's.
+        ix->built = false;
+        ix->dev.vshift = knobs().bag_vs >= 2 && knobs().bag_vs <= wave_vshift(ix->dev.cap < kWaveMaxN ? ix->dev.cap : kWaveMaxN)
+                             ? knobs().bag_vs : wave_vshift(N);
+        rc = launch_bag_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, (int)N,
+                              ctx_error_word(ctx));
+        if (rc) return rc;
+        record_build(ix, true, indices, itype, table_stride, index_base, batch, lookups);
+        ix->dev.has_map = 1;
+        return DLRM_OK;
+    }
     ix->dev.vshift = build_vshift(ix, N, split);
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, lookups,
                               split);
@@ -797,11 +810,9 @@ int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb,
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_prepare: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_prepare: batch %d > capacity %lld", batch, (long long)ix->dev.cap);
     const int vs = wave_parts_log2(batch);
-    if (batch > kWaveMaxN || tb->T + 1 > 32 || (1 << vs) > indexer_parts(ix->dev.cap))
-        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d, %d tables (the wave build: batch <= %d, "
-                        "<= 31 tables)", batch, tb->T, kWaveMaxN);
-    rc = ensure_parts(ctx, ix, vs);
-    if (rc) return rc;
+    if (!wave_fits(ix, batch))
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d (the wave build: batch <= %d, "
+                        "tables x capacity < 2^31)", batch, kWaveMaxN);
     ix->built = false;
     ix->prepared = false;
     ix->dev.vshift = vs;
@@ -831,7 +842,12 @@ static int read_indexer_table(dlrm_ctx* ctx, const dlrm_indexer* ix, int v, Inde
     int rc = ctx_hip(ctx, hipMemcpy(cnt, ix->dev.counts + (int64_t)v * 8, sizeof(cnt), hipMemcpyDeviceToHost), "read");
     if (rc) return rc;
     const int64_t U = cnt[0], NV = cnt[4];
-    const int64_t off = (int64_t)v * ix->dev.cap;
+    // (a wave build's parts are packed per table: IndexerDev::part_off / seg_off)
+    const int vs = ix->dev.vshift;
+    const int64_t cap = ix->dev.cap;
+    const int64_t off = ix->dev.has_map ? (int64_t)(v >> vs) * cap + cnt[kCntOff] : (int64_t)v * cap;
+    const int64_t soff = ix->dev.has_map ? (int64_t)(v >> vs) * (cap + kSegPad) + cnt[kCntOff] + (v & ((1 << vs) - 1))
+                                         : (int64_t)v * (cap + 1);
     o.rows.resize(U);
     o.perm.resize(NV);
     o.seg_start.resize(U + 1);
@@ -839,7 +855,7 @@ static int read_indexer_table(dlrm_ctx* ctx, const dlrm_indexer* ix, int v, Inde
     if (rc == DLRM_OK && NV)
         rc = ctx_hip(ctx, hipMemcpy(o.perm.data(), ix->dev.perm + off, NV * 4, hipMemcpyDeviceToHost), "read");
     if (rc == DLRM_OK)
-        rc = ctx_hip(ctx, hipMemcpy(o.seg_start.data(), ix->dev.seg_start + (int64_t)v * (ix->dev.cap + 1),
+        rc = ctx_hip(ctx, hipMemcpy(o.seg_start.data(), ix->dev.seg_start + soff,
                                     (U + 1) * 4, hipMemcpyDeviceToHost), "read");
     return rc;
 }
@@ -964,7 +980,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     ix->prepared = false;
     ix->built = false;
     // the wave build in the forward's launch (vshift >= 2: it also writes the apply's item map)
-    ix->dev.vshift = has_parts(ix, wave_parts_log2(kStepIndexMaxN)) ? wave_parts_log2(kStepIndexMaxN) : 0;
+    ix->dev.vshift = ix->dev.cap <= kWaveApplyMaxN && wave_fits(ix, batch) ? wave_parts_log2(kStepIndexMaxN) : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev, tb->h_desc.data());
     if (rc == DLRM_OK) {
@@ -1097,8 +1113,8 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     // forward's split build (the same parts), so the next dlrm_step_fwd only gathers
     const int NB = (tb->T + 1 + 15) / 16;
     // (the split backward's shapes only: the apply launch that carries the build has no once-hit items)
-    const bool inapply = batch > 0 && tb->T > 0 && batch <= kWaveMaxN && NB <= 2 && tb->aligned16 &&
-                         (1 << wave_parts_log2(batch)) <= indexer_parts(next->dev.cap) &&
+    const bool inapply = batch > 0 && tb->T > 0 && batch <= kWaveApplyMaxN && NB <= 2 && tb->aligned16 &&
+                         wave_fits(next, batch) &&
                          step_split_supported(tb->aligned16, tb->T, tb->dtype, tb->D, x, x_ld);
     if (!inapply)  // no pipelined form for this shape: the plain step (the next forward builds)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
@@ -1106,8 +1122,6 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     if (flags & DLRM_STEP_BWD_ONLY)  // (the next build rides on the apply launch)
         return step_bwd_impl(ctx, tb, ix, indices, itype, table_stride, index_base, batch, x, x_ld, dout, dout_ld,
                              padding, dx, dx_ld, dt, dt_ld, lr, flags, nullptr);
-    rc = ensure_parts(ctx, next, wave_parts_log2(batch) < 2 ? 2 : wave_parts_log2(batch));
-    if (rc) return rc;
     next->built = false;
     next->prepared = false;
     // the wave build: 2^wave_parts_log2(batch) parts per table, one wave each (4 per workgroup)

@@ -228,16 +228,24 @@ constexpr int kHixMaxN = 1 << 20;   // hash indexer (hashindex.hip): positions p
 constexpr int kStepIndexMaxN = 2048;  // the forward-launch indexer (interact.hip): positions per table
 constexpr int kStepMaxParts = 16;     // ... which sorts a table as up to 16 parts (by the row's low bits)
 // the wave build (indexer.hpp wave_build_group) of the next batch (in the apply launch) or of a
-// prepared batch (dlrm_indexer_prepare): up to kWaveMaxN positions per table, as 16 parts per 2048
-// positions (2^wave_vshift(N) parts per table; a part averages <= 128 positions)
-constexpr int kWaveMaxN = 16384;
+// prepared batch (dlrm_indexer_prepare, and dlrm_indexer_build's pooled bags): up to kWaveMaxN
+// positions per table, as 16 parts per 2048 positions (2^wave_vshift(N) parts per table; a part
+// averages <= 128 positions).  The in-apply build (dlrm_step_bwd_prepare) takes up to
+// kWaveApplyMaxN (its scan build keeps a quarter of the table's indices in registers).
+constexpr int kWaveMaxN = 32768;
+constexpr int kWaveApplyMaxN = 16384;
+constexpr int kWaveMaxVshift = 8;
 __host__ __device__ constexpr int wave_vshift(int64_t N) {
-    return N <= 2048 ? 4 : (N <= 4096 ? 5 : (N <= 8192 ? 6 : 7));
+    return N <= 2048 ? 4 : (N <= 4096 ? 5 : (N <= 8192 ? 6 : (N <= 16384 ? 7 : 8)));
 }
-// virtual tables per table an indexer of `cap` positions per table provides (its per-part arrays)
-__host__ __device__ constexpr int indexer_parts(int64_t cap) {
-    return cap <= kWaveMaxN ? (1 << wave_vshift(cap)) : 1;
-}
+// The wave builds' per-part arrays are packed per table (round 6, "compact" layout): part q of
+// table t (virtual table v = (t << vs) + q) keeps its entries at t * cap + off_q, off_q = the
+// table's positions in parts < q (IndexerDev::counts[v][CNT_OFF]); its segment starts at
+// t * (cap + kSegPad) + off_q + q (one sentinel per part).  So an indexer of cap positions per table
+// holds any wave build in T * cap slots, whatever the parts (the old layout gave every part a whole
+// cap: 128 x the table at 16384 positions).
+constexpr int kSegPad = 1 << kWaveMaxVshift;
+constexpr int kCntOff = 5;  // counts[v][kCntOff]: the part's offset in its table (wave builds)
 // the next batch's split build in the apply launch (indexer.hpp wave_build_group): parts per
 // table, one wave each, 4 per workgroup (>= 4)
 #ifndef DLRM_WAVE_PARTS
@@ -305,10 +313,21 @@ struct IndexerDev {
     // prebuilt update without one)
     const unsigned* build_err;
     int chunk_max;         // the wave build's chunk limit (16 or 32; indexer.hpp kMinChunk .. kChunk)
-    int has_map;
+    int has_map;           // 1: a wave build (flat item map, compact per-part layout)
     int64_t cap;
     int64_t pcap;          // slices per table (upper bound)
     int pdim;              // partial row capacity (elements)
+
+    // where virtual table v's per-part entries (perm, seg_row, hot, hot_slice; chunks at twice it)
+    // and its segment starts begin: packed per table after a wave build (has_map), else v * cap
+    __device__ __forceinline__ int64_t part_off(int v) const {
+        return has_map ? (int64_t)(v >> vshift) * cap + counts[(int64_t)v * 8 + kCntOff] : (int64_t)v * cap;
+    }
+    __device__ __forceinline__ int64_t seg_off(int v) const {
+        return has_map ? (int64_t)(v >> vshift) * (cap + kSegPad) + counts[(int64_t)v * 8 + kCntOff] +
+                             (v & ((1 << vshift) - 1))
+                       : (int64_t)v * (cap + 1);
+    }
 };
 int64_t indexer_slice_cap(int64_t cap);
 constexpr int kPartialDim = 256;  // partial rows allocated with the indexer (larger D: regrown on use)
@@ -339,6 +358,9 @@ struct Knobs {
     int upd_sbu;      // DLRM_UPD_SBU (1/2): super-blocks in flight in the one-wave step backward
     int wave_rounds;  // DLRM_WAVE_ROUNDS=1: the wave build in rounds above 2048 positions per table
                       // instead of the scan build
+    int bag_hash;     // DLRM_BAG_WAVE=0: dlrm_indexer_build of 8192 < N <= 32768 positions per table (pooled
+                      // bags) by the hash build instead of the bag build
+    int bag_vs;       // DLRM_BAG_VS (2..8): the bag build's log2 parts per table (default wave_vshift(N))
 };
 const Knobs& knobs();
 
@@ -393,6 +415,8 @@ int launch_scatter_rows(dlrm_ctx* ctx, int esize, int T, int B, int D, const voi
 int launch_indexer_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx,
                          int itype, int64_t tstride, int base, int B, int L, bool split = false,
                          hipStream_t stream = nullptr);
+int launch_bag_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
+                     int64_t tstride, int base, int N, unsigned* err);
 int launch_step_prepare(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T, const void* idx, int itype,
                         int64_t tstride, int base, int N, unsigned* err);
 struct SinglesArgs;

@@ -25,7 +25,7 @@ constexpr int kChunk = DLRM_CHUNK;  // max positions of a segment handled by one
 // group.  kMinChunk bounds the slice counts the allocations are sized for.
 constexpr int kMinChunk = 16;
 constexpr int kRankBucketMax = 64;  // within-bucket rank sort when every bucket is this small
-enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4 };
+enum { CNT_U = 0, CNT_C = 1, CNT_H = 2, CNT_S = 3, CNT_NV = 4, CNT_OFF = kCntOff };
 // Hot segments are cut into slices of kHotSlice positions, one work item (one 256-thread apply
 // workgroup: 8 lane groups x 16 rows in flight at D = 128, two rounds) each, so a hot row's grad rows are read
 // by several CUs at once; a segment of several slices is combined by its last-arriving slice (sc1
@@ -643,6 +643,9 @@ struct WaveBuildLds {
     // [round][wave][part]: positions of the workgroup's part q that wave w read in round r (a round
     // = 2048 positions, 512 per wave)
     int tot[kWaveMaxN / kStepIndexMaxN][kWaveParts][kWaveParts];
+    // per wave: the table's positions it read that fall in parts below the workgroup's (q < q0),
+    // whose sum places the workgroup's parts in the table's compact region (common.hpp kSegPad)
+    int below[16];
 };
 // the scan build's per-wave counts of its four parts (<= 16 waves), in the rounds form's tot array
 __device__ __forceinline__ int4* scan_wave_totals(WaveBuildLds& sl) { return (int4*)&sl.tot[0][0][0]; }
@@ -656,8 +659,12 @@ static_assert(sizeof(WaveBuildLds::tot) >= 16 * sizeof(int4), "tot holds the sca
 // at most cap / 2 chunks and as many slices); item_tot[j] / [kResLists + j] = its slices / chunks.
 constexpr int kResSliceShift = 24, kResArriveShift = 44;
 constexpr int kResLists = 8, kResWordStride = 32;  // (u64 words: 256 B apart)
-__host__ __device__ __forceinline__ int res_stride(int groups, int64_t cap) {
-    return ((groups + kResLists - 1) / kResLists) * (int)(cap / 2 + 8);
+// (a sub-list's records also number at most half its positions: <= T0 cap / 2, T0 = the real
+// tables, which bounds it once the parts outnumber 32 per table)
+__host__ __device__ __forceinline__ int res_stride(int groups, int64_t cap, int vs) {
+    const int64_t per_group = ((groups + kResLists - 1) / kResLists) * (cap / 2 + 8);
+    const int64_t per_table = (int64_t)((groups * kWaveParts) >> vs) * (cap / 2 + 8);
+    return (int)(per_group < per_table ? per_group : per_table);
 }
 // flat record index of item k of the sub-lists with counts cnt[0..kResLists), or -1 past the end
 __device__ __forceinline__ int res_locate(const int* cnt, int k, int stride) {
@@ -851,7 +858,8 @@ struct SegPass {
     const uint32_t* Ks;
     const int32_t* Vs;
     const int32_t* R;
-    int64_t off;
+    int64_t off;   // the part's per-part entries (compact: t * cap + its offset in the table)
+    int64_t soff;  // its segment starts
 
     // segments [s0, s0 + 64): the per-part lists (seg_start, seg_row, chunks, hot, hot_slice) when
     // `lists`, and this lane's flat record; c / h / sl0 run over the tiles
@@ -885,7 +893,7 @@ struct SegPass {
         }
         if (lists) {
             if (ok) {
-                ix.seg_start[(int64_t)v * (ix.cap + 1) + s] = beg;
+                ix.seg_start[soff + s] = beg;
                 ix.seg_row[off + s] = (uint32_t)row;
             }
             if (isc) {
@@ -968,6 +976,64 @@ __device__ __forceinline__ void wave_sort_regs(int n, int nbits, const uint32_t*
     else wave_sort_regs_r<4, uint32_t>(n, K0, V0, K1, V1);
 }
 
+// A part of n > 256 keys dominated by one hot row (Zipf rows: a pooled table's hottest row takes
+// ~18 % of its 20480 positions, all in one part): the wave picks the most frequent key of a
+// 64-key sample, counts it (nh), and when the other n - nh keys fit the register sort, partitions
+// the part stably -- the hot row's positions to the front of (K0, V0) in place (they come in
+// position order: a segment as it is), the others to (K1, V1)[nh, n) -- and sorts those in
+// registers back into (K0, V0)[nh, n).  Returns false (nothing written) otherwise: the caller
+// sorts the part the general way.  The same cost whatever the hot row's share, instead of the
+// counting passes' serial walk over every key of the hot bucket.
+template <bool G>
+__device__ __forceinline__ bool bag_hot_sort(int n, int nbits, uint32_t* K0, int32_t* V0, uint32_t* K1, int32_t* V1) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t mine = K0[(int64_t)lane * n / 64];
+    int c = 0;
+    for (int j = 0; j < 64; ++j) c += __shfl(mine, j, 64) == mine ? 1 : 0;
+    int best = (c << 6) | lane;  // the most frequent sample key (ties: highest lane)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off, 64));
+    const uint32_t hkey = __shfl(mine, best & 63, 64);
+    int nh = 0;
+    for (int i0 = 0; i0 < n; i0 += 256) {  // (four tiles' loads in flight)
+        uint32_t k[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) k[u] = i0 + 64 * u + lane < n ? K0[i0 + 64 * u + lane] : ~hkey;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) nh += __popcll(__ballot(k[u] == hkey));
+    }
+    if (!regsort_takes(n - nh, nbits) && n - nh > 1) return false;
+    const unsigned long long below = lanes_below();
+    int hrun = 0, rrun = nh;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const bool ok = i < n;
+        const uint32_t k = ok ? K0[i] : 0u;
+        const int32_t p = ok ? V0[i] : 0;
+        const bool hot = ok && k == hkey;
+        const unsigned long long hb = __ballot(hot), rb = __ballot(ok && !hot);
+        if (hot) {  // (in place: i >= hrun + rank, and every lane has read its entry)
+            K0[hrun + __popcll(hb & below)] = hkey;
+            V0[hrun + __popcll(hb & below)] = p;
+        } else if (ok) {
+            K1[rrun + __popcll(rb & below)] = k;
+            V1[rrun + __popcll(rb & below)] = p;
+        }
+        hrun += __popcll(hb);
+        rrun += __popcll(rb);
+    }
+    part_sync<G>();
+    if (n - nh > 1) {
+        wave_sort_regs(n - nh, nbits, K1 + nh, V1 + nh, K0 + nh, V0 + nh);
+        part_sync<G>();
+    } else if (n - nh == 1 && lane == 0) {
+        K0[nh] = K1[nh];
+        V0[nh] = V1[nh];
+    }
+    part_sync<G>();
+    return true;
+}
+
 // The part the calling wave sorts and writes out: virtual table v = (t << vs) + part, its n keys
 // (row >> vs) and positions in position order at K0 / V0 (K1, V1, R: the same span of the pool's
 // other arrays, scratch).  Sorts them in LDS: keys wider than 8 bits by one unstable counting pass
@@ -977,9 +1043,11 @@ __device__ __forceinline__ void wave_sort_regs(int n, int nbits, const uint32_t*
 // DIRECT: a part of one row (its table has <= 2^vs rows): the caller already wrote perm (positions in
 // order) and the once-hit flags; K0 / V0 hold the part's first (up to 8) keys / positions and R room
 // for one segment start -- the part is one segment, nothing is sorted.
-template <bool G, bool DIRECT = false>
-__device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n, uint32_t* K0,
-                               int32_t* V0, uint32_t* K1, int32_t* V1, int32_t* R, uint32_t* cnt, int g, int groups) {
+// PRESORTED: (K0, V0) already hold the part grouped by row (bag_hot_sort); only the pass below runs.
+template <bool G, bool DIRECT = false, bool PRESORTED = false>
+__device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n,
+                                               int toff, uint32_t* K0, int32_t* V0, uint32_t* K1, int32_t* V1,
+                                               int32_t* R, uint32_t* cnt, int g, int groups) {
     const int lane = threadIdx.x & 63;
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
     const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
@@ -987,7 +1055,7 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
-    if (DIRECT) {
+    if (DIRECT || PRESORTED) {
     } else if (!G && regsort_takes(n, nbits)) {  // (uniform: n, nbits)
         WPH(3);
         wave_sort_regs(n, nbits, K0, V0, K1, V1);
@@ -1017,10 +1085,11 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     // slices are counted from R after.  (Its stores precede the reservation atomic below; they
     // complete before it returns anyway.)
     const int cm = ix.chunk_max;  // this build's chunk limit (16 or 32)
-    const int64_t off = (int64_t)v * ix.cap;
+    const int64_t off = (int64_t)t * ix.cap + toff;  // (the compact layout, common.hpp)
+    const int64_t soff = (int64_t)t * (ix.cap + kSegPad) + toff + (int)part;
     int32_t* perm = ix.perm + off;
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
-    const bool pvec = (ix.cap & 3) == 0;  // perm + i 16-B aligned
+    const bool pvec = (off & 3) == 0;  // perm + i 16-B aligned
     int U = 0, C = 0, H = 0;
     if (DIRECT) {
         U = n > 0 ? 1 : 0;
@@ -1096,16 +1165,16 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     WPH(9);
     // segments: the first two tiles keep their flat records in registers for after the reservation
     // returns; later tiles (U > 128) are recomputed then
-    SegPass sp{ix, v, vs, part, n, U, Ks, Vs, R, off};
+    SegPass sp{ix, v, vs, part, n, U, Ks, Vs, R, off, soff};
     int c = 0, h = 0, sl0 = 0;
     const SegRec r0 = sp.tile(0, c, h, sl0, true);
     const SegRec r1 = U > 64 ? sp.tile(64, c, h, sl0, true) : SegRec{};
     const int c2 = c, s2 = sl0;
     for (int s0 = 128; s0 < U; s0 += 64) (void)sp.tile(s0, c, h, sl0, true);
     if (lane == 0) {
-        ix.seg_start[(int64_t)v * (ix.cap + 1) + U] = n;
+        ix.seg_start[soff + U] = n;
         int32_t* cn = ix.counts + (int64_t)v * 8;
-        cn[CNT_U] = U; cn[CNT_C] = c; cn[CNT_H] = h; cn[CNT_S] = sl0; cn[CNT_NV] = n;
+        cn[CNT_U] = U; cn[CNT_C] = c; cn[CNT_H] = h; cn[CNT_S] = sl0; cn[CNT_NV] = n; cn[CNT_OFF] = toff;
     }
     // the reservation's return: the wave's bases in its sub-list; the sub-list's last wave to arrive
     // publishes its totals and clears the word for this indexer's next build (read in a later launch)
@@ -1120,7 +1189,7 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
         ix.item_tot[kResLists + list] = cloc + C;
         *word = 0ull;
     }
-    const int lbase = list * res_stride(groups, ix.cap);
+    const int lbase = list * res_stride(groups, ix.cap, vs);
     const int cbase = lbase + cloc, sbase = lbase + sloc;
     // the flat records (chunk_rec, slice_rec) at the reserved ranges
     sp.flat(r0, cbase, sbase);
@@ -1147,6 +1216,7 @@ struct WaveRound {
     uint32_t rv[8];
     uint32_t code;
     bool bad;
+    int below;  // this lane's positions in parts below q0 (the compact layout's table offset)
     int pre[2][kWaveParts], ptot[2][kWaveParts];
 };
 
@@ -1189,11 +1259,13 @@ __device__ __forceinline__ void wave_round_decode(WaveRound& o, const WaveRaw& r
     WPH(7);
     o.code = 0;
     o.bad = false;
+    o.below = 0;
 #pragma unroll
     for (int j = 0; j < 4 * PK; ++j) {
         const int64_t x = raw.rr[j] - base;
         const bool ok = raw.in[j] && (uint64_t)x < (uint64_t)nrows;  // (negative: a huge unsigned)
         o.bad |= raw.in[j] && !ok;
+        o.below += ok && ((uint32_t)x & pmask) < (uint32_t)q0 ? 1 : 0;
         const uint32_t pq = ((uint32_t)x & pmask) - (uint32_t)q0;
         o.code |= (ok && pq < (uint32_t)kWaveParts ? pq : 4u) << (3 * j);
         o.rv[j] = (uint32_t)x >> vs;
@@ -1216,104 +1288,6 @@ __device__ __forceinline__ void wave_round_decode(WaveRound& o, const WaveRaw& r
     }
 }
 
-// ------------------------------------ wave build, N <= 2048, without the exchange (round 6, NOT used)
-// Measured slower and kept only as an A/B form (-DDLRM_WAVE_SCAN_SMALL): the standalone build's
-// loads ended at 2.2 us instead of 1.2 (each wave issues 4x the loads, lane-contiguous so every
-// load instruction touches 64 lines) and the branchy per-element placement took 2.6 us, against
-// 1.2 + 0.7 us for the exchange + barrier below; inside the apply launch the step's apply went
-// 11 -> 23.5 us (the build waves' extra VALU work beside the apply waves).
-// One build workgroup = parts q0 .. q0 + 3 of table t, one wave each, as below; but every wave
-// reads ALL of the table's N positions itself -- lane l the 4·E4 consecutive positions
-// [4·E4·l, 4·E4·(l + 1)), E4 = ceil(N / 256) 16-B loads (<= 8 KB per wave, from L2 after the
-// first) -- counts the workgroup's four parts (two DPP scans of 16-bit counters packed in pairs:
-// each lane's exclusive prefix per part, the wave's totals = the parts' sizes, hence the pool
-// regions), and appends only its OWN part's (key, position) pairs, in position order.  The four
-// waves exchange nothing: no workgroup barrier waits for the slowest wave's loads (round 5's
-// rounds form: counts + barrier 1.3 us, placement 0.9 us after the loads, p50).
-__device__ __forceinline__ void wave_build_group_small(const IndexerDev& ix, int g, int T,
-                                                       const TableDesc* __restrict__ tabs, const void* __restrict__ idx,
-                                                       int itype, int64_t tstride, int base, int N,
-                                                       unsigned* __restrict__ err, WaveBuildLds& sl) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
-    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
-    const uint32_t nrows = (uint32_t)load_table(tabs, t).nrows;
-    const uint32_t pmask = (1u << vs) - 1u;
-    constexpr uint32_t kBad = 0xffffffffu;  // (no row: nrows <= 2^32 - 1)
-    WPH(0);
-    constexpr int ME4 = kStepIndexMaxN / 256;
-    const int E4 = (N + 255) >> 8;
-    const int p0 = lane * 4 * E4;
-    const int32_t* i32 = (const int32_t*)idx + (int64_t)t * tstride;
-    const bool vec = itype == DLRM_I32 && (N & 3) == 0 && ((uintptr_t)i32 & 15) == 0;
-    uint32_t xv[4 * ME4];  // row - base, or kBad (past N or out of range)
-    bool bad = false;
-    if (vec) {
-        int4 q[ME4];
-#pragma unroll
-        for (int j = 0; j < ME4; ++j) {
-            if (j < E4 && p0 + 4 * j < N) q[j] = ldg<int4>(i32 + p0 + 4 * j);
-            else q[j] = make_int4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < ME4; ++j) {
-            const bool in = j < E4 && p0 + 4 * j < N;
-            const int e4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t x = (int64_t)e4[e] - base;
-                const bool ok = in && (uint64_t)x < (uint64_t)nrows;
-                bad |= in && !ok;
-                xv[4 * j + e] = ok ? (uint32_t)x : kBad;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4 * ME4; ++j) {
-            const bool in = j < 4 * E4 && p0 + j < N;
-            const int64_t x = load_index_if(in, idx, itype, (int64_t)t * tstride + p0 + j) - base;
-            const bool ok = in && (uint64_t)x < (uint64_t)nrows;
-            bad |= in && !ok;
-            xv[j] = ok ? (uint32_t)x : kBad;
-        }
-    }
-    WPH(7);
-    // out of range raises BoundsError; wave 0 of the workgroup of parts 0..3 reports it
-    if (q0 == 0 && w == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
-    // the workgroup's four parts: per lane counts, two 16-bit fields per word (<= 2048 per wave)
-    int c01 = 0, c23 = 0;
-#pragma unroll
-    for (int j = 0; j < 4 * ME4; ++j) {
-        const uint32_t q = xv[j] == kBad ? 4u : (xv[j] & pmask) - (uint32_t)q0;  // (>= 4: not this workgroup's)
-        c01 += q == 0u ? 1 : (q == 1u ? 0x10000 : 0);
-        c23 += q == 2u ? 1 : (q == 3u ? 0x10000 : 0);
-    }
-    const int i01 = wave_incl_scan(c01), i23 = wave_incl_scan(c23);
-    const int t01 = lane63(i01), t23 = lane63(i23);
-    const int n_of[kWaveParts] = {t01 & 0xffff, t01 >> 16, t23 & 0xffff, t23 >> 16};
-    int pb = 0;  // this wave's pool region: parts in order, 16-B aligned (wave_sort_part's vector reads)
-#pragma unroll
-    for (int q = 0; q < kWaveParts; ++q) pb += q < w ? (n_of[q] + 3) & ~3 : 0;
-    const int e01 = i01 - c01, e23 = i23 - c23;
-    int at = pb + (w == 0 ? e01 & 0xffff : w == 1 ? e01 >> 16 : w == 2 ? e23 & 0xffff : e23 >> 16);
-#pragma unroll
-    for (int j = 0; j < 4 * ME4; ++j) {
-        const uint32_t q = xv[j] == kBad ? 4u : (xv[j] & pmask) - (uint32_t)q0;
-        if (q == (uint32_t)w) {
-            sl.K[0][at] = xv[j] >> vs;
-            sl.V[0][at] = p0 + j;
-            ++at;
-        }
-    }
-    wave_lds_sync();
-    WPH(1);
-    const int n = n_of[w];
-    const int v = (t << vs) + q0 + w;
-    const int groups = (T << vs) / kWaveParts;
-    wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
-                          sl.cnt[w], g, groups);
-}
-
 // One build workgroup (kWaveParts waves = 256 threads): parts q0 .. q0 + 3 (q0 = 4 (g mod P / 4))
 // of table t = g / (P / 4), P = 2^vs >= 4 parts per table.  Every thread of the workgroup calls
 // it.  The four waves first split the table's positions among the four parts together -- in rounds
@@ -1328,15 +1302,9 @@ __device__ __forceinline__ void wave_build_group_small(const IndexerDev& ix, int
 // BIG = false: N <= 2048 (one round, the pool never overflows) -- the forward launch's build, whose
 // registers the HBM path would crowd; BIG = true: any N <= kWaveMaxN.
 template <bool BIG = true>
-__device__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
+__device__ __forceinline__ void wave_build_group(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
                                  const void* __restrict__ idx, int itype, int64_t tstride, int base, int N,
                                  unsigned* __restrict__ err, WaveBuildLds& sl) {
-#ifdef DLRM_WAVE_SCAN_SMALL  // (tried, slower: every wave reading the whole table, see above)
-    if constexpr (!BIG) {
-        wave_build_group_small(ix, g, T, tabs, idx, itype, tstride, base, N, err, sl);
-        return;
-    }
-#endif
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;  // workgroups per table
     const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
@@ -1345,6 +1313,7 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     WPH(0);
     WaveRound rd;
     bool bad = false;
+    int blw = 0;  // positions of parts below q0 this lane read
     // BIG with 16-B int32 index loads: rounds in batches of RB, each batch's loads issued together
     // (one latency per batch, not per round); otherwise round by round
     constexpr int RB = BIG ? 2 : 1;
@@ -1375,6 +1344,7 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     };
     auto count_round = [&](int r) {  // pass 1's bookkeeping of round r (rd decoded)
         bad |= rd.bad;
+        blw += rd.below;
         if (lane < kWaveParts) {
             int tw = 0;
 #pragma unroll
@@ -1402,10 +1372,15 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     }
     // out of range raises BoundsError; the workgroup of parts 0..3 reports it
     if (q0 == 0 && __ballot(bad) && lane == 0) raise_index_error(err);
+    blw = lane63(wave_incl_scan(blw));
+    if (lane == 0) sl.below[w] = blw;
     __syncthreads();
-    // part q's size, its region (pool: 16-B aligned, in part order; HBM: its own virtual table's),
-    // and the offset of each round's share of wave w in it
-    int n_of[kWaveParts], pbase[kWaveParts], total = 0;
+    // part q's size, its region (pool: 16-B aligned, in part order; HBM: its compact region), the
+    // offset of each round's share of wave w in it, and its offset in the table's compact region
+    int n_of[kWaveParts], pbase[kWaveParts], toff[kWaveParts], total = 0;
+    int tq = 0;
+#pragma unroll
+    for (int ww = 0; ww < kWaveParts; ++ww) tq += sl.below[ww];
 #pragma unroll
     for (int q = 0; q < kWaveParts; ++q) {
         int nq = 0;
@@ -1414,6 +1389,8 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
             for (int ww = 0; ww < kWaveParts; ++ww) nq += sl.tot[r][ww][q];
         n_of[q] = nq;
         pbase[q] = total;
+        toff[q] = tq;
+        tq += nq;
         total += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
     }
     // a table of <= 2^vs rows: every part is one row (DIRECT: positions go straight to perm in order,
@@ -1453,17 +1430,23 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
                         if (cd == (uint32_t)q) dst = at[q]++;
                     const int32_t pos = kStepIndexMaxN * r + (kStepIndexMaxN / kWaveParts) * w + 256 * k + 4 * lane + e;
                     if (direct) {  // the part's perm entry and the position's once-hit flag, now
-                        int nq = 0;
+                        int nq = 0, to = 0;
 #pragma unroll
-                        for (int q = 0; q < kWaveParts; ++q) nq = cd == (uint32_t)q ? n_of[q] : nq;
-                        ix.perm[(int64_t)((t << vs) + q0 + (int)cd) * ix.cap + dst] = pos;
+                        for (int q = 0; q < kWaveParts; ++q) {
+                            nq = cd == (uint32_t)q ? n_of[q] : nq;
+                            to = cd == (uint32_t)q ? toff[q] : to;
+                        }
+                        ix.perm[(int64_t)t * ix.cap + to + dst] = pos;
                         ix.single[(int64_t)t * ix.cap + pos] = nq == 1 ? 1 : 0;
                         if (dst < 8) {  // (the part's first positions: its chunk record carries 5 inline)
                             sl.K[0][8 * (int)cd + dst] = rd.rv[4 * k + e];
                             sl.V[0][8 * (int)cd + dst] = pos;
                         }
                     } else if (G) {
-                        const int64_t vo = (int64_t)((t << vs) + q0 + (int)cd) * ix.cap + dst;
+                        int to = 0;
+#pragma unroll
+                        for (int q = 0; q < kWaveParts; ++q) to = cd == (uint32_t)q ? toff[q] : to;
+                        const int64_t vo = (int64_t)t * ix.cap + to + dst;
                         ix.wscratch[vo] = rd.rv[4 * k + e];
                         ((int32_t*)ix.wscratch)[ix.wstride + vo] = pos;
                     } else {
@@ -1500,17 +1483,17 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
     const int v = (t << vs) + q0 + w;
     const int groups = (T << vs) / kWaveParts;
     if (BIG && direct) {
-        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, sl.K[0] + 8 * w, sl.V[0] + 8 * w, sl.K[1] + 8 * w,
-                                    sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
+        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, toff[w], sl.K[0] + 8 * w, sl.V[0] + 8 * w,
+                                    sl.K[1] + 8 * w, sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
     } else if (BIG && G) {
-        uint32_t* K0 = ix.wscratch + (int64_t)v * ix.cap;
+        uint32_t* K0 = ix.wscratch + (int64_t)t * ix.cap + toff[w];
         const int64_t S = ix.wstride;
-        wave_sort_part<true>(ix, v, t, vs, nrows, n, K0, (int32_t*)(K0 + S), K0 + 2 * S, (int32_t*)(K0 + 3 * S),
-                             (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
+        wave_sort_part<true>(ix, v, t, vs, nrows, n, toff[w], K0, (int32_t*)(K0 + S), K0 + 2 * S,
+                             (int32_t*)(K0 + 3 * S), (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
     } else {
         const int pb = pbase[w];
-        wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb,
-                              sl.R + pb, sl.cnt[w], g, groups);
+        wave_sort_part<false>(ix, v, t, vs, nrows, n, toff[w], sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb,
+                              sl.V[1] + pb, sl.R + pb, sl.cnt[w], g, groups);
     }
 }
 
@@ -1518,22 +1501,22 @@ __device__ void wave_build_group(const IndexerDev& ix, int g, int T, const Table
 // sorts part q0 + w of table t -- n positions placed at pool offset pb, in HBM scratch (G), or
 // already in perm (direct).
 __device__ __forceinline__ void wave_build_sort(const IndexerDev& ix, int g, int T, int t, int q0, int vs,
-                                                uint32_t nrows, int n, int pb, bool direct, bool G,
+                                                uint32_t nrows, int n, int toff, int pb, bool direct, bool G,
                                                 WaveBuildLds& sl) {
     const int w = threadIdx.x >> 6;
     const int v = (t << vs) + q0 + w;
     const int groups = (T << vs) / kWaveParts;
     if (direct) {
-        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, sl.K[0] + 8 * w, sl.V[0] + 8 * w, sl.K[1] + 8 * w,
-                                    sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
+        wave_sort_part<false, true>(ix, v, t, vs, nrows, n, toff, sl.K[0] + 8 * w, sl.V[0] + 8 * w,
+                                    sl.K[1] + 8 * w, sl.V[1] + 8 * w, sl.R + 8 * w, sl.cnt[w], g, groups);
     } else if (G) {
-        uint32_t* K0 = ix.wscratch + (int64_t)v * ix.cap;
+        uint32_t* K0 = ix.wscratch + (int64_t)t * ix.cap + toff;
         const int64_t S = ix.wstride;
-        wave_sort_part<true>(ix, v, t, vs, nrows, n, K0, (int32_t*)(K0 + S), K0 + 2 * S, (int32_t*)(K0 + 3 * S),
-                             (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
+        wave_sort_part<true>(ix, v, t, vs, nrows, n, toff, K0, (int32_t*)(K0 + S), K0 + 2 * S,
+                             (int32_t*)(K0 + 3 * S), (int32_t*)(K0 + 4 * S), sl.cnt[w], g, groups);
     } else {
-        wave_sort_part<false>(ix, v, t, vs, nrows, n, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb, sl.V[1] + pb,
-                              sl.R + pb, sl.cnt[w], g, groups);
+        wave_sort_part<false>(ix, v, t, vs, nrows, n, toff, sl.K[0] + pb, sl.V[0] + pb, sl.K[1] + pb,
+                              sl.V[1] + pb, sl.R + pb, sl.cnt[w], g, groups);
     }
 }
 
@@ -1556,8 +1539,8 @@ __device__ __forceinline__ void wave_build_sort(const IndexerDev& ix, int g, int
 // is a chain of dependent VALU / DPP steps, so more waves shorten it: the standalone build runs 16
 // waves per workgroup (4 per SIMD; waves 4 .. 15 leave before the sort), the in-apply build 4.  Needs
 // int32 indices, 16-B aligned per table, N % 4 == 0 (else the rounds form runs).
-template <int NW>
-__device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
+template <int NW, int MAXN = kWaveApplyMaxN>
+__device__ __forceinline__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const TableDesc* __restrict__ tabs,
                                       const void* __restrict__ idx, int64_t tstride, int base, int N,
                                       unsigned* __restrict__ err, WaveBuildLds& sl) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1569,7 +1552,8 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
     const int Q = ((N + NW * 256 - 1) / (NW * 256)) * 256;  // positions per wave (whole pieces)
     const int pw0 = w * Q;
     const int npc = pw0 < N ? (min(pw0 + Q, N) - pw0 + 255) / 256 : 0;  // this wave's pieces
-    constexpr int MP = kWaveMaxN / NW / 256;                          // (16 / NW = 4, 4 / NW = 16)
+    constexpr int MP = MAXN / NW / 256;  // pieces per wave (<= 16: mbits; 16384 / 16 waves: 4, / 4: 16)
+    static_assert(MP >= 1 && MP <= 16 && MAXN <= kWaveMaxN, "scan build: <= 16 pieces per wave");
     WPH(0);
     int4 v[MP];
 #pragma unroll
@@ -1581,6 +1565,7 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
     uint32_t acc = 0;
     uint64_t mbits = 0;
     bool bad = false;
+    int blw = 0;  // positions of parts below q0 (the compact layout's table offset)
 #pragma unroll
     for (int u = 0; u < MP; ++u) {
         // (a guard, not a break: a loop with two exits is not unrolled, and v[] would go to scratch)
@@ -1593,6 +1578,7 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
             bad |= in && !ok;
             const uint32_t pq = (x & pmask) - (uint32_t)q0;
             const bool m = ok && pq < (uint32_t)kWaveParts;
+            blw += ok && (x & pmask) < (uint32_t)q0 ? 1 : 0;
             acc += m ? 1u << (8 * pq) : 0u;
             mbits |= m ? 1ull << (4 * u + e) : 0ull;
         }
@@ -1602,13 +1588,19 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
         const int a = (int)((acc & 0xffu) | (((acc >> 8) & 0xffu) << 16));
         const int b = (int)(((acc >> 16) & 0xffu) | ((acc >> 24) << 16));
         const int ta = lane63(wave_incl_scan(a)), tb = lane63(wave_incl_scan(b));
-        if (lane == 0) scan_wave_totals(sl)[w] = make_int4(ta & 0xffff, ta >> 16, tb & 0xffff, tb >> 16);
+        const int tbl = lane63(wave_incl_scan(blw));
+        if (lane == 0) {
+            scan_wave_totals(sl)[w] = make_int4(ta & 0xffff, ta >> 16, tb & 0xffff, tb >> 16);
+            sl.below[w] = tbl;
+        }
     }
     __syncthreads();
-    int n_of[kWaveParts], pbase[kWaveParts], at0[kWaveParts], total = 0, sbase = 0;
+    int n_of[kWaveParts], pbase[kWaveParts], at0[kWaveParts], toff[kWaveParts], total = 0, sbase = 0;
     int4 nall = make_int4(0, 0, 0, 0), nbef = make_int4(0, 0, 0, 0);
+    int tq = 0;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) {
+        tq += sl.below[ww];
         const int4 c = scan_wave_totals(sl)[ww];
         nall = make_int4(nall.x + c.x, nall.y + c.y, nall.z + c.z, nall.w + c.w);
         if (ww < w) nbef = make_int4(nbef.x + c.x, nbef.y + c.y, nbef.z + c.z, nbef.w + c.w);
@@ -1619,6 +1611,8 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
         const int before = q == 0 ? nbef.x : (q == 1 ? nbef.y : (q == 2 ? nbef.z : nbef.w));
         n_of[q] = nq;
         pbase[q] = total;
+        toff[q] = tq;
+        tq += nq;
         at0[q] = before;
         sbase += before;
         total += (nq + 3) & ~3;  // (16-B aligned regions: wave_sort_part's vector reads)
@@ -1712,15 +1706,16 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
             for (int e = 0; e < 4; ++e) {
                 if (cd[e] >= (uint32_t)kWaveParts) continue;
                 const int q = (int)cd[e];
-                int dst = 0, nq = 0;
+                int dst = 0, nq = 0, to = 0;
 #pragma unroll
                 for (int x = 0; x < kWaveParts; ++x)
                     if (q == x) {
                         dst = at[x]++;
                         nq = n_of[x];
+                        to = toff[x];
                     }
                 const int32_t pos = p + e;
-                const int64_t vo = (int64_t)((t << vs) + q0 + q) * ix.cap + dst;
+                const int64_t vo = (int64_t)t * ix.cap + to + dst;
                 if (direct) {  // the part's perm entry and the position's once-hit flag, now
                     ix.perm[vo] = pos;
                     ix.single[(int64_t)t * ix.cap + pos] = nq == 1 ? 1 : 0;
@@ -1740,7 +1735,7 @@ __device__ void wave_build_group_scan(const IndexerDev& ix, int g, int T, const 
     if (G) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (w >= kWaveParts) return;  // (NW > 4: the extra waves only scanned; the sort has no barrier)
     WPH(7);
-    wave_build_sort(ix, g, T, t, q0, vs, nrows, n_of[w], pbase[w], direct, G, sl);
+    wave_build_sort(ix, g, T, t, q0, vs, nrows, n_of[w], toff[w], pbase[w], direct, G, sl);
 }
 
 }  // namespace dlrm

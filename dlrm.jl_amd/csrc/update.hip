@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
             Stot += ls[j];
             Ctot += lc[j];
         }
-        lstride = res_stride(T_ / kWaveParts, ix.cap);
+        lstride = res_stride(T_ / kWaveParts, ix.cap, ix.vshift);
     } else {
         sS = scan_counts(ix, T_, CNT_S);
         sC = scan_counts(ix, T_, CNT_C);
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(kApplyThreads, 3) void sgd_apply_kernel(IndexerDev 
                 ca = ix.chunk_rec[2 * (int64_t)r];
                 cb = ix.chunk_rec[2 * (int64_t)r + 1];
                 pbase = ix.perm;
-                t = (int)(ca.x / ix.cap) >> ix.vshift;
+                t = (int)(ca.x / ix.cap);  // (the compact layout: entries of table t at [t cap, (t + 1) cap))
             } else {
                 int tc, cl;
                 locate(ix, T_, CNT_C, sC, fc, tc, cl);
@@ -563,20 +563,20 @@ __global__ __launch_bounds__(256) void step_index_kernel(PrepArgs pa) {
 // The scan build alone (indexer.hpp wave_build_group_scan), NW waves per workgroup: 16 when every
 // workgroup is resident at once (one per CU: its ~94 registers allow 20 waves per CU), else 8 (two
 // per CU) -- a second round of workgroups would double the build.
-template <int NW>
+template <int NW, int MAXN>
 __global__ __launch_bounds__(64 * NW) void step_index_scan_kernel(PrepArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    wave_build_group_scan<NW>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.tstride, pa.base, pa.N, pa.err,
+    wave_build_group_scan<NW, MAXN>(pa.ix, blockIdx.x, pa.T, pa.tabs, pa.idx, pa.tstride, pa.base, pa.N, pa.err,
                               *(WaveBuildLds*)lds);
 }
 
-template <int NW>
+template <int NW, int MAXN = kWaveApplyMaxN>
 static void launch_step_index_scan(hipStream_t s, const PrepArgs& pa) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_scan_kernel<NW>,
+    static const hipError_t attr = hipFuncSetAttribute((const void*)step_index_scan_kernel<NW, MAXN>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)sizeof(WaveBuildLds));
     (void)attr;
-    hipLaunchKernelGGL(step_index_scan_kernel<NW>, dim3((unsigned)prep_groups(pa)), dim3(64 * NW),
+    hipLaunchKernelGGL((step_index_scan_kernel<NW, MAXN>), dim3((unsigned)prep_groups(pa)), dim3(64 * NW),
                        sizeof(WaveBuildLds), s, pa);
 }
 
@@ -605,8 +605,217 @@ static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
     const int kind = pa.N <= kStepIndexMaxN ? 0 : wave_big_kind(pa);
     if (kind == 0) launch_step_index_kind<0>(s, pa);
     else if (kind == 1) launch_step_index_kind<1>(s, pa);
+    else if (pa.N > kWaveApplyMaxN)  // (pooled bags: 64 tables x 20480; 16 waves keep 8 pieces each in registers)
+        launch_step_index_scan<16, kWaveMaxN>(s, pa);
     else if (prep_groups(pa) <= pa_cus(pa)) launch_step_index_scan<16>(s, pa);
     else launch_step_index_scan<8>(s, pa);
+}
+
+// ---------------------------------------------------------------- bag build (8192 < N <= 32768)
+// dlrm_indexer_build of many positions per table (configs[4]'s pooled bags: 64 tables x 20480,
+// p = b L + k) as three short launches, partition first, so no workgroup reads more than its own
+// share of the indices (the scan build reads the whole table once per 4 parts: 64 times at 256
+// parts, 183 us for configs[4]; the hash build it replaces took 146 us with 13x its algorithmic
+// bytes in global atomics):
+//   1. count: one workgroup per 2048-position chunk of a table: each valid position's part
+//      (row & (P - 1), P = 2^wave_vshift(N)) counted in LDS; the chunk's P counts -> keys0
+//      [T][chunks][P].  Out-of-range indices raise the bounds flag and are left out.
+//   2. place: the same chunks again; each workgroup sums the count matrix of its table into the
+//      parts' sizes and offsets (the compact layout: part q at the table's positions in parts < q,
+//      kept in counts[v][CNT_OFF] / [kCntN]) and its chunk's base in every part, then writes each
+//      position as (row >> vs, position) to its part in the HBM scratch (wscratch K0 / V0), in
+//      position order: waves take consecutive quarters of the chunk, tiles of 64 in order, lanes
+//      of one part ranked by ballots (match_digit), one cursor per (wave, part) in LDS.
+//   3. sort: the wave build's last step (wave_sort_part), one wave per part, 4 per workgroup: a
+//      part of <= 512 positions is copied into its quarter of the LDS pool and sorted there (in
+//      registers up to 256 keys), a larger one (hot rows) in the HBM scratch; then segments,
+//      once-hit flags and the flat item lists, exactly as every wave build's.
+constexpr int kBagChunk = 2048;    // positions per count / place workgroup
+constexpr int kBagLdsPart = 512;   // a part sorted in LDS (its quarter of the pool), else in HBM
+constexpr int kCntN = 6;           // counts[v][kCntN]: the part's size from the count matrix
+
+__global__ __launch_bounds__(256) void bag_count_kernel(PrepArgs pa, int nch) {
+    __shared__ int hist[kSegPad];
+    const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x;
+    const int P = 1 << pa.ix.vshift;
+    const uint32_t pmask = (uint32_t)P - 1u;
+    for (int q = tid; q < P; q += 256) hist[q] = 0;
+    __syncthreads();
+    const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
+    const int p0 = c * kBagChunk;
+    int64_t x[kBagChunk / 256];
+    bool in[kBagChunk / 256];
+#pragma unroll
+    for (int i = 0; i < kBagChunk / 256; ++i) {  // (every load in flight)
+        const int p = p0 + i * 256 + tid;
+        in[i] = p < pa.N;
+        x[i] = load_index_if(in[i], pa.idx, pa.itype, (int64_t)t * pa.tstride + p) - pa.base;
+    }
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < kBagChunk / 256; ++i) {
+        const bool ok = in[i] && (uint64_t)x[i] < nrows;
+        bad |= in[i] && !ok;
+        if (ok) atomicAdd(&hist[(uint32_t)x[i] & pmask], 1);
+    }
+    if (__ballot(bad) && (tid & 63) == 0) raise_index_error(pa.err);
+    __syncthreads();
+    int32_t* cg = (int32_t*)pa.ix.keys0 + ((int64_t)t * nch + c) * P;
+    for (int q = tid; q < P; q += 256) cg[q] = hist[q];
+}
+
+__global__ __launch_bounds__(256) void bag_place_kernel(PrepArgs pa, int nch) {
+    __shared__ int cw[kWaveParts][kSegPad];  // per-wave counts, then per-wave cursors in the chunk
+    __shared__ int cb[kSegPad];              // part q's entries of this chunk start at cb[q] (table)
+    __shared__ int cl[kSegPad];              // ... and at cl[q] in the chunk's staging
+    __shared__ uint32_t sx[kBagChunk];       // the chunk grouped by part: rows, positions
+    __shared__ int32_t sp[kBagChunk];
+    __shared__ int wtot[8];
+    const IndexerDev& ix = pa.ix;
+    const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    const int vs = ix.vshift, P = 1 << vs;
+    const uint32_t pmask = (uint32_t)P - 1u;
+    // part q = tid: its size over the table's chunks and the positions of earlier chunks in it
+    const int32_t* cg = (const int32_t*)ix.keys0 + (int64_t)t * nch * P;
+    int nq = 0, bef = 0, here = 0;
+    if (tid < P)
+        for (int cc = 0; cc < nch; ++cc) {
+            const int k = cg[(int64_t)cc * P + tid];
+            nq += k;
+            bef += cc < c ? k : 0;
+            here = cc == c ? k : here;
+        }
+    int total;
+    const int toff = block_scan_nw<kWaveParts, int>(tid < P ? nq : 0, wtot, &total);
+    const int loff = block_scan_nw<kWaveParts, int>(tid < P ? here : 0, wtot, &total);
+    if (tid < P) {
+        cb[tid] = toff + bef;
+        cl[tid] = loff;
+        if (c == 0) {
+            int32_t* cn = ix.counts + ((int64_t)(t << vs) + tid) * 8;
+            cn[CNT_OFF] = toff;
+            cn[kCntN] = nq;
+        }
+    }
+    for (int q = tid; q < kWaveParts * kSegPad; q += 256) (&cw[0][0])[q] = 0;
+    __syncthreads();
+    // pass 1: this wave's positions per part (its quarter of the chunk, kept in registers)
+    const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
+    constexpr int IT = kBagChunk / 256;  // tiles of 64 per wave
+    constexpr uint32_t kBad = 0xffffffffu;
+    const int pw = c * kBagChunk + w * (kBagChunk / kWaveParts);
+    uint32_t xr[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const int p = pw + i * 64 + lane;
+        const bool in = p < pa.N;
+        const int64_t x = load_index_if(in, pa.idx, pa.itype, (int64_t)t * pa.tstride + p) - pa.base;
+        xr[i] = in && (uint64_t)x < nrows ? (uint32_t)x : kBad;
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+        if (xr[i] != kBad) atomicAdd(&cw[w][xr[i] & pmask], 1);
+    __syncthreads();
+    if (tid < P) {  // cursors: part q's start in the staging, then the earlier waves' shares
+        int run = cl[tid];
+#pragma unroll
+        for (int ww = 0; ww < kWaveParts; ++ww) {
+            const int k = cw[ww][tid];
+            cw[ww][tid] = run;
+            run += k;
+        }
+    }
+    __syncthreads();
+    // pass 2: the chunk into the staging, grouped by part, position order within a part (tiles in
+    // order, the lanes of one part ranked by lane)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const bool ok = xr[i] != kBad;
+        const uint32_t q = xr[i] & pmask;
+        const unsigned long long peers = match_digit(q, ok, vs);
+        const int rank = __popcll(peers & lanes_below());
+        const int base = ok ? cw[w][q] : 0;
+        if (ok && rank == 0) cw[w][q] = base + __popcll(peers);
+        if (ok) {
+            sx[base + rank] = xr[i];
+            sp[base + rank] = pw + i * 64 + lane;
+        }
+    }
+    __syncthreads();
+    // out: consecutive staged entries of one part go to consecutive slots of its region
+    uint32_t* K0 = ix.wscratch + (int64_t)t * ix.cap;
+    int32_t* V0 = (int32_t*)ix.wscratch + ix.wstride + (int64_t)t * ix.cap;
+    const int m = cw[kWaveParts - 1][P - 1];  // entries staged (the last wave's cursor of the last part)
+    for (int i = tid; i < m; i += 256) {
+        const uint32_t x = sx[i];
+        const uint32_t q = x & pmask;
+        const int dst = cb[q] + (i - cl[q]);
+        K0[dst] = x >> vs;
+        V0[dst] = sp[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void bag_sort_kernel(PrepArgs pa) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    WaveBuildLds& sl = *(WaveBuildLds*)lds;
+    const IndexerDev& ix = pa.ix;
+    const int g = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;
+    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const int v = (t << vs) + q0 + w;
+    const int groups = (pa.T << vs) / kWaveParts;
+    const uint32_t nrows = (uint32_t)load_table(pa.tabs, t).nrows;
+    const int n = ix.counts[(int64_t)v * 8 + kCntN], toff = ix.counts[(int64_t)v * 8 + CNT_OFF];
+    const int64_t S = ix.wstride, o = (int64_t)t * ix.cap + toff;
+    uint32_t* K0 = ix.wscratch + o;
+    int32_t* V0 = (int32_t*)ix.wscratch + S + o;
+    const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
+    const int nbits = 32 - __clz(kmax);
+    if (n <= kBagLdsPart) {
+        const int pb = w * (kBagLdsPart + 4);  // (16-B aligned quarters of the pool)
+        uint32_t* LK0 = sl.K[0] + pb;
+        int32_t* LV0 = sl.V[0] + pb;
+        for (int i = lane; i < n; i += 64) {
+            LK0[i] = K0[i];
+            LV0[i] = V0[i];
+        }
+        wave_lds_sync();
+        if (n > kRegSortMax && nbits > 0 && bag_hot_sort<false>(n, nbits, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb))
+            wave_sort_part<false, false, true>(ix, v, t, vs, nrows, n, toff, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb,
+                                               sl.R + pb, sl.cnt[w], g, groups);
+        else
+            wave_sort_part<false>(ix, v, t, vs, nrows, n, toff, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
+                                  sl.cnt[w], g, groups);
+    } else {
+        uint32_t* K1 = ix.wscratch + 2 * S + o;
+        int32_t* V1 = (int32_t*)ix.wscratch + 3 * S + o;
+        int32_t* R = (int32_t*)ix.wscratch + 4 * S + o;
+        if (nbits > 0 && bag_hot_sort<true>(n, nbits, K0, V0, K1, V1))
+            wave_sort_part<true, false, true>(ix, v, t, vs, nrows, n, toff, K0, V0, K1, V1, R, sl.cnt[w], g, groups);
+        else
+            wave_sort_part<true>(ix, v, t, vs, nrows, n, toff, K0, V0, K1, V1, R, sl.cnt[w], g, groups);
+    }
+}
+static_assert(kWaveParts * (kBagLdsPart + 4) <= kStepIndexMaxN + 16, "bag sort: four quarters of the pool");
+
+int launch_bag_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs, int T_, const void* idx, int itype,
+                     int64_t tstride, int base, int N, unsigned* err) {
+    if (T_ == 0 || N == 0) return DLRM_OK;
+    const int nch = (N + kBagChunk - 1) / kBagChunk;
+    if (ix.vshift < 2 || ix.vshift > kWaveMaxVshift || ix.wstride <= 0 || (int64_t)nch * (1 << ix.vshift) > ix.cap)
+        return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "bag build: N %d, vshift %d, capacity %lld", N, ix.vshift,
+                        (long long)ix.cap);
+    const PrepArgs pa{ix, tabs, T_, idx, itype, tstride, base, N, err};
+    hipStream_t s = ctx_stream(ctx);
+    hipLaunchKernelGGL(bag_count_kernel, dim3((unsigned)nch, (unsigned)T_), dim3(256), 0, s, pa, nch);
+    hipLaunchKernelGGL(bag_place_kernel, dim3((unsigned)nch, (unsigned)T_), dim3(256), 0, s, pa, nch);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)bag_sort_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)sizeof(WaveBuildLds));
+    (void)attr;
+    hipLaunchKernelGGL(bag_sort_kernel, dim3((unsigned)prep_groups(pa)), dim3(256), sizeof(WaveBuildLds), s, pa);
+    return ctx_hip(ctx, hipGetLastError(), "bag build launch");
 }
 
 // The step's split build alone (dlrm_indexer_prepare): the wave build + item lists, 4 parts per
@@ -631,7 +840,7 @@ __global__ __launch_bounds__(256) void sgd_chunks_scalar(IndexerDev ix, TableDes
     if (*err) return;
     const int t = blockIdx.y;
     const int nchunks = ix.counts[(int64_t)t * 8 + CNT_C];
-    const int64_t off = (int64_t)t * ix.cap;
+    const int64_t off = ix.part_off(t);
     const int64_t total = (int64_t)nchunks * D;
     TT* table = (TT*)tabs[t >> ix.vshift].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -652,7 +861,7 @@ __global__ __launch_bounds__(256) void sgd_hot_scalar(IndexerDev ix, TableDesc* 
     if (*err) return;
     const int t = blockIdx.y;
     const int nhot = ix.counts[(int64_t)t * 8 + CNT_H];
-    const int64_t off = (int64_t)t * ix.cap;
+    const int64_t off = ix.part_off(t);
     const int64_t total = (int64_t)nhot * D;
     TT* table = (TT*)tabs[t >> ix.vshift].data;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {

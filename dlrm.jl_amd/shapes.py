@@ -41,7 +41,7 @@ WORKLOADS = {
 }
 
 
-WAVE_MAX_N = 16384  # the wave build's positions per table (csrc/common.hpp kWaveMaxN)
+WAVE_MAX_N = 32768  # the wave build's positions per table (csrc/common.hpp kWaveMaxN)
 # One GPU: the in-apply wave build, and the side stream's wave build, up to APPLY_MAX_N positions per
 # table; above, the side stream's in-LDS parts build (configs[2] at 8192: 85.3 M samples/s, against
 # 69 M with the scan build in the apply launch and 82 M with it on the side stream, round 5).  The

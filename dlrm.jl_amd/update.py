@@ -112,8 +112,8 @@ class SparseIndexer:
         return self
 
     def prepare(self, tables, indices, *, index_base=1):
-        """The training step's split build of `indices` (one-hot, <= 16384 positions per table, <= 31
-        tables) as its own launch (dlrm_indexer_prepare: the wave build): a following dlrm_step_fwd of
+        """The training step's split build of `indices` (one-hot, <= 32768 positions per table) as its
+        own launch (dlrm_indexer_prepare: the wave build): a following dlrm_step_fwd of
         these indices only gathers, and update_ / dlrm_sgd_update(PREBUILT) take its once-hit
         positions as well.  Returns False where the wave build does not apply (use build())."""
         ts = as_table_set(tables)
@@ -130,8 +130,8 @@ class SparseIndexer:
         return True
 
     def reserve(self, batch):
-        """Re-carves the indexer for wave builds of `batch` positions per table now (dlrm_indexer_reserve),
-        so that a graph capture with its first such build does not have to (the capture refuses it)."""
+        """dlrm_indexer_reserve: a no-op since round 6 (the wave builds' packed layout needs no
+        re-carving before a graph capture); kept for round-5 callers."""
         self.ctx.check(self.ctx.lib.dlrm_indexer_reserve(self.ctx.bind(), self.handle, int(batch)))
         return self
 
@@ -141,7 +141,7 @@ class SparseIndexer:
         return self
 
     def nbytes(self):
-        """Device bytes held (dlrm_indexer_bytes: grows on the first wave build of > 2048 positions)."""
+        """Device bytes held (dlrm_indexer_bytes: all allocated at creation, never grown)."""
         b = ctypes.c_int64()
         self.ctx.check(self.ctx.lib.dlrm_indexer_bytes(self.handle, ctypes.byref(b)))
         return b.value

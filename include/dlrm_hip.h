@@ -242,11 +242,11 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
 
 /* The training step's split build of `indices` on the ctx's stream -- a side stream: it depends on
  * the indices only -- so that the dlrm_step_fwd of the same indices only gathers (the build
- * dlrm_step_bwd_prepare runs inside an apply launch, as its own launch).  One-hot, batch <= 16384
+ * dlrm_step_bwd_prepare runs inside an apply launch, as its own launch).  One-hot, batch <= 32768
  * positions per table (16 table parts per 2048 positions, one wave each; above 2048 positions the
  * scan build: 8 or 16 waves per workgroup scan the table, int32 indices with 16-B aligned tables and
- * batch % 4 == 0, else the build in rounds), <= 31 tables; the indexer
- * must have been created for >= batch positions.  Replaces the SparseIndexer() build of
+ * batch % 4 == 0, else the build in rounds), any number of tables (tables x capacity < 2^31); the
+ * indexer must have been created for >= batch positions.  Replaces the SparseIndexer() build of
  * train.jl:276-281 ahead of the step (also the table-sharded update's build over the global
  * batch).  Out-of-range indices are left out of the build and raise the ctx's bounds flag through
  * the lookup / forward of the same indices, or the apply of this indexer (dlrm_sgd_update PREBUILT,
@@ -256,16 +256,14 @@ int dlrm_indexer_read(dlrm_ctx* ctx, const dlrm_indexer* indexer, int table,
 int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
                          const void* indices, int itype, int64_t table_stride, int index_base, int batch);
 
-/* Device bytes the indexer holds.  It is created with the per-part arrays of the builds up to 2048
- * positions per table (16 parts per table: ~92 B x 16 x cap per table, plus the item lists and, above
- * 4096, the hash arrays); the first wave build of more positions (dlrm_indexer_prepare,
- * dlrm_step_bwd_prepare; 2^k parts per table, 16 per 2048 positions) re-carves it with that many
- * parts -- ~112 B x 128 x 16384 = 235 MB per table at 16384 positions -- so run one such build
- * before graph capture (inside a capture it returns DLRM_E_ARG). */
+/* Device bytes the indexer holds, all allocated by dlrm_indexer_create: the per-part arrays (~92 B
+ * per position slot; the wave builds pack a table's parts back to back, so any of them fits cap
+ * slots per table -- x 8 for a cap of 4097..8192, the in-LDS parts build's layout), the wave
+ * build's flat item lists (<= 256 B per slot) and HBM sort scratch (20 B, cap > 2048), and above
+ * 4096 the hash arrays.  Nothing grows on a later build (26 tables x 16384: ~0.2 GB). */
 int dlrm_indexer_bytes(const dlrm_indexer* indexer, int64_t* bytes);
-/* Re-carves the indexer now for wave builds of `batch` positions per table (no-op when it already
- * has that layout or batch <= 2048): call it before capturing a graph whose first wave build
- * of > 2048 positions would otherwise re-carve it inside the capture. */
+/* Kept for callers of round 5's layout, which re-carved the indexer on its first wave build of
+ * > 2048 positions: the packed layout needs no re-carving, so this only validates batch. */
 int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* indexer, int batch);
 /* The wave build's chunk limit for this indexer's later builds (16 or 32, default 32): segments of
  * at most this many positions become chunk items (one lane group each), longer ones hot-slice items

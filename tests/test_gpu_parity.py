@@ -274,18 +274,24 @@ def test_step_fwd_indexer_parts(pkg, gpu, rows, B, zipf):
     ([1], 16384, None, ""), ([0x10000, 0x1000000], 3000, None, ""), ([7, 70000], 2049, None, ""),
     ([1000], 16384, None, "one-part"),                                 # every index in one part: 8 rows
     ([5000, 3], 4100, 1.05, ""),
-    ([300, 100000, 3, 5_000_000], 6000, 1.1, "int64")])               # int64 indices: the rounds form
+    ([300, 100000, 3, 5_000_000], 6000, 1.1, "int64"),                # int64 indices: the rounds form
+    ([3, 1000, 40, 5_000_000], 32768, None, ""),                      # 256 parts per table (scan, 16 waves)
+    ([1_000_000] * 3, 20480, 1.2, ""),                                 # configs[4]'s positions, Zipf hot rows
+    ([70000, 9], 30000, 1.05, "int64"),                               # 32768-class rounds form (16 rounds)
+    ([1000], 32768, None, "one-part")])                               # every index in one part of 256
 def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
     """dlrm_indexer_prepare (the wave build: 16 parts per 2048 positions; above 2048 the scan build --
     int32 indices, N % 4 == 0 -- else rounds of 2048 positions; parts that overflow a workgroup's LDS
-    pool sorted in HBM) up to 16384 positions per table: unique rows and per-row positions exactly
-    numpy's, every once-hit flag right."""
+    pool sorted in HBM) up to 32768 positions per table: unique rows and per-row positions exactly
+    numpy's, every once-hit flag right.  The parts of a table are packed back to back (round 6's
+    compact layout: each part's entries at its table's offset + the positions of the parts below it)."""
     if rows == "kaggle":
         rows = pkg.KAGGLE_EMBEDDING_SIZES
     rng = np.random.default_rng(B + len(rows) + 3)
     idx = rand_indices(rng, rows, B, 1, zipf=zipf)
-    if case == "one-part":  # rows 5 + 128 k: all in part 5 of 128
-        idx = (5 + 128 * rng.integers(0, 7, size=(1, B))).astype(idx.dtype)
+    if case == "one-part":  # rows 5 + P k: all in part 5 of P (128 at 16384, 256 at 32768)
+        P = 128 if B <= 16384 else 256
+        idx = (5 + P * rng.integers(0, 1000 // P, size=(1, B))).astype(idx.dtype)
     tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B, gpu)
     itype = torch.int64 if case == "int64" else torch.int32
@@ -405,6 +411,51 @@ def test_prepared_step_equals_fresh_step_and_bounds(pkg, gpu):
         hp2.check_bounds()
     for t in range(len(rows)):
         assert np.array_equal(to_np_f32(hp2.ts[t].data), tabs[t]), f"table {t} was written on a BoundsError step"
+
+
+@pytest.mark.parametrize("rows,B,L,zipf", [
+    ([1_000_000] * 6, 2048, 10, 1.2),          # configs[4]'s bags: 20480 positions per table, Zipf(1.2)
+    ([3, 1000, 40, 5_000_000], 3000, 8, None),  # 24000: tiny tables (one row per part: DIRECT), uniform
+    ([7, 100_000], 4096, 8, 1.05),              # 32768: the largest wave build
+    ([1_000_000] * 2, 1000, 9, 1.2)])           # 9000: N % 256 != 0
+def test_bag_wave_build_segments(pkg, gpu, rows, B, L, zipf):
+    """dlrm_indexer_build of pooled bags with 8192 < B L <= 32768 positions per table: the wave scan
+    build (round 6; it replaced the hash build for configs[4]) groups the positions p = b L + k
+    exactly as numpy does; then a prebuilt update_ (the apply maps p to its bag) equals the
+    closed-form scatter-add of integer bag gradients on every touched row, and writes no other row."""
+    rng = np.random.default_rng(B * L + len(rows))
+    idx = rand_indices(rng, rows, B, L, zipf=zipf)
+    D = 16
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, D), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B * L, gpu)
+    p = pkg.PackedIndices(torch.from_numpy(idx).to(torch.int32).to(gpu).reshape(len(rows), B, L))
+    ix.build(tabs, p, index_base=0)
+    tabs.ctx.check_bounds()
+    _assert_segments(ix, idx, B * L)
+    gi = torch.from_numpy(rng.integers(-4, 5, size=(B, len(rows) * D)).astype(np.float32)).to(gpu)
+    pkg.update_(pkg.Descent(1.0), tabs, pkg.maplookup_pullback(0, tabs, p, gi), ix, index_base=0, prebuilt=True)
+    gh = gi.cpu().numpy()
+    for t, n in enumerate(rows):
+        ref = np.zeros((n, D), dtype=np.float64)
+        np.add.at(ref, idx[t], np.repeat(gh[:, t * D:(t + 1) * D], L, axis=0))
+        assert np.array_equal(to_np_f32(tabs[t].data), (-ref).astype(np.float32))
+
+
+def test_indexer_footprint_compact(pkg, gpu):
+    """the wave builds' per-part arrays are packed per table (round 6), so an indexer of
+    26 tables x 16384 positions holds its 128-part build in a few hundred bytes per position
+    (round 5: ~7 GB after the first such build), and it does not grow when that build runs."""
+    rows = pkg.KAGGLE_EMBEDDING_SIZES
+    N = 16384
+    ix = pkg.SparseIndexer(len(rows), N, gpu)
+    before = ix.nbytes()
+    assert before < len(rows) * N * 600, before
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, 16), device=gpu) for n in rows])
+    idx = rand_indices(np.random.default_rng(3), rows, N, 1)
+    assert ix.prepare(tabs, torch.from_numpy(idx).to(torch.int32).to(gpu), index_base=0)
+    tabs.ctx.check_bounds()
+    assert ix.nbytes() == before
+    _assert_segments(ix, idx, N)
 
 
 def _assert_segments(ix, idx, N):
