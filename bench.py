@@ -696,6 +696,16 @@ def main():
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: sbwd_k(k, pkg._lib.STEP_BWD_ONLY),
                    apply_prep_k]
             bytes_["sgd_update"] += bytes_["indexer_build"]
+        elif engine.pipeline and L > 1:  # pooled bags: the next batch's bag build beside the apply
+            names = ["lookup_interact_fwd", "interact_bwd", "sgd_update", "indexer_build"]
+
+            def build_k(k):
+                engine.indexer = indexers[k]
+                engine.build_indexer(packs[k])
+                engine.indexer = home
+
+            fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: engine.interact_bwd(dout, x=x, idx=packs[k]),
+                   apply_k, build_k]
         elif engine.pipeline:  # indexer on the side stream, built for the next batch
             names = ["lookup_interact_fwd", "interact_bwd", "sgd_update", "indexer_build"]
             fns = [lambda k: engine.lookup_interact_fwd(x, packs[k]), lambda k: sbwd_k(k, pkg._lib.STEP_BWD_ONLY),

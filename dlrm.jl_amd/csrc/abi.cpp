@@ -768,8 +768,11 @@ int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb, c
         // p = b L + k; the apply maps p to its bag.  Bounds errors go to the ctx's flag, as every
         // dlrm_indexer_build's.
         ix->built = false;
+        // half the parts of the wave builds (128 to 256 positions per part; configs[4] at 20480: 128
+        // parts, 50.6 us against 66.7 us with 256 -- half the sort workgroups, each still sorting in
+        // registers)
         ix->dev.vshift = knobs().bag_vs >= 2 && knobs().bag_vs <= wave_vshift(ix->dev.cap < kWaveMaxN ? ix->dev.cap : kWaveMaxN)
-                             ? knobs().bag_vs : wave_vshift(N);
+                             ? knobs().bag_vs : wave_vshift(N) - 1;
         rc = launch_bag_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, (int)N,
                               ctx_error_word(ctx));
         if (rc) return rc;

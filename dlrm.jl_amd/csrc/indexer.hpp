@@ -860,6 +860,8 @@ struct SegPass {
     const int32_t* R;
     int64_t off;   // the part's per-part entries (compact: t * cap + its offset in the table)
     int64_t soff;  // its segment starts
+    int kb = 0;          // > 0: segment 0 is a hot-row prefix of kb positions (key hkey, not in Ks / Vs,
+    uint32_t hkey = 0;   // which hold the part's entries from kb on: entry i at Ks[i - kb])
 
     // segments [s0, s0 + 64): the per-part lists (seg_start, seg_row, chunks, hot, hot_slice) when
     // `lists`, and this lane's flat record; c / h / sl0 run over the tiles
@@ -876,14 +878,14 @@ struct SegPass {
         const int ns = ish ? (len + kHotSlice - 1) / kHotSlice : 0;
         const unsigned long long cb = __ballot(isc), hb = __ballot(ish);
         const int sincl = wave_incl_scan(ns);
-        const int row = ok ? (int)((Ks[beg] << vs) | part) : 0;
+        const int row = ok ? (int)(((kb > 0 && s == 0 ? hkey : Ks[beg - kb]) << vs) | part) : 0;
         SegRec r{};
         r.kind = isc ? 1 : (ish ? 2 : 0);
         r.ns = ns;
         if (isc) {
             int q[kChunkInline];
 #pragma unroll
-            for (int k = 0; k < kChunkInline; ++k) q[k] = beg + k < end ? Vs[beg + k] : -1;
+            for (int k = 0; k < kChunkInline; ++k) q[k] = beg + k < end ? Vs[beg + k - kb] : -1;
             r.idx = c + __popcll(cb & lt);
             r.a = make_int4((int)off + beg, (int)off + end, row, q[0]);
             r.b = make_int4(q[1], q[2], q[3], q[4]);
@@ -1044,10 +1046,13 @@ __device__ __forceinline__ bool bag_hot_sort(int n, int nbits, uint32_t* K0, int
 // order) and the once-hit flags; K0 / V0 hold the part's first (up to 8) keys / positions and R room
 // for one segment start -- the part is one segment, nothing is sorted.
 // PRESORTED: (K0, V0) already hold the part grouped by row (bag_hot_sort); only the pass below runs.
+// nh0 > 0 (PRESORTED only): the part's first nh0 entries are one hot row's (key hkey) whose perm
+// entries and once-hit flags the caller has written; (K0, V0) hold the other n - nh0, grouped.
 template <bool G, bool DIRECT = false, bool PRESORTED = false>
 __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int t, int vs, uint32_t nrows, int n,
                                                int toff, uint32_t* K0, int32_t* V0, uint32_t* K1, int32_t* V1,
-                                               int32_t* R, uint32_t* cnt, int g, int groups) {
+                                               int32_t* R, uint32_t* cnt, int g, int groups, int nh0 = 0,
+                                               uint32_t hkey = 0) {
     const int lane = threadIdx.x & 63;
     const uint32_t part = (uint32_t)v & ((1u << vs) - 1u);
     const uint32_t kmax = nrows > 0 ? (nrows - 1) >> vs : 0u;
@@ -1055,23 +1060,24 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     WPH(2);
     const uint32_t* Ks = K0;
     const int32_t* Vs = V0;
+    const int nr = n - nh0;  // (the entries in K0 / V0: all but a hot prefix)
     if (DIRECT || PRESORTED) {
-    } else if (!G && regsort_takes(n, nbits)) {  // (uniform: n, nbits)
+    } else if (!G && regsort_takes(nr, nbits)) {  // (uniform: n, nbits)
         WPH(3);
-        wave_sort_regs(n, nbits, K0, V0, K1, V1);
+        wave_sort_regs(nr, nbits, K0, V0, K1, V1);
         Ks = K1;
         Vs = V1;
-    } else if (n > 1 && nbits > 8 && wave_count_pass_unstable<G>(n, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
+    } else if (nr > 1 && nbits > 8 && wave_count_pass_unstable<G>(nr, K0, V0, K1, V1, R, cnt) <= kWaveRankMax) {
         WPH(3);
-        wave_rank_buckets<G>(n, K1, V1, K0, V0, cnt);
-    } else if (n > 1 && nbits > 0) {  // narrow keys, or skewed rows: stable LSD passes from (K0, V0)
-        wave_count_pass<G>(n, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
+        wave_rank_buckets<G>(nr, K1, V1, K0, V0, cnt);
+    } else if (nr > 1 && nbits > 0) {  // narrow keys, or skewed rows: stable LSD passes from (K0, V0)
+        wave_count_pass<G>(nr, 0, nbits < 8 ? nbits : 8, K0, V0, K1, V1, R, cnt);
         WPH(3);
         Ks = K1;
         Vs = V1;
         for (int shift = 8; shift < nbits; shift += 8) {
             const bool from1 = Ks == K1;
-            wave_count_pass<G>(n, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
+            wave_count_pass<G>(nr, shift, nbits - shift < 8 ? nbits - shift : 8, from1 ? K1 : K0, from1 ? V1 : V0,
                             from1 ? K0 : K1, from1 ? V0 : V1, R, cnt);
             Ks = from1 ? K0 : K1;
             Vs = from1 ? V0 : V1;
@@ -1087,17 +1093,18 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     const int cm = ix.chunk_max;  // this build's chunk limit (16 or 32)
     const int64_t off = (int64_t)t * ix.cap + toff;  // (the compact layout, common.hpp)
     const int64_t soff = (int64_t)t * (ix.cap + kSegPad) + toff + (int)part;
-    int32_t* perm = ix.perm + off;
+    int32_t* perm = ix.perm + off + nh0;
     uint8_t* single = ix.single + (int64_t)t * ix.cap;
-    const bool pvec = (off & 3) == 0;  // perm + i 16-B aligned
+    const bool pvec = ((off + nh0) & 3) == 0;  // perm + i 16-B aligned
     int U = 0, C = 0, H = 0;
-    if (DIRECT) {
-        U = n > 0 ? 1 : 0;
-        C = n >= 2 && n <= cm ? 1 : 0;
-        H = n > cm ? 1 : 0;
+    if (DIRECT || nh0 > 0) {  // (one segment already written: the whole part, or the hot prefix)
+        const int n1 = DIRECT ? n : nh0;
+        U = n1 > 0 ? 1 : 0;
+        C = n1 >= 2 && n1 <= cm ? 1 : 0;
+        H = n1 > cm ? 1 : 0;
         if (lane == 0) R[0] = 0;
     }
-    for (int j0 = 0; j0 < (DIRECT ? 0 : n); j0 += 256) {
+    for (int j0 = 0; j0 < (DIRECT ? 0 : nr); j0 += 256) {
         const int i = j0 + 4 * lane;
         const uint4 k4 = *(const uint4*)(Ks + i);  // (past n: garbage, masked below)
         const int4 v4 = *(const int4*)(Vs + i);
@@ -1111,29 +1118,29 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int ie = i + e;
-            const bool ok = ie < n;
+            const bool ok = ie < nr;
             const bool head = ok && (ie == 0 || kk[e] != kk[e + 1]);
-            const bool tail = ok && (ie + 1 == n || kk[e + 2] != kk[e + 1]);
-            const bool longer = ok && ie + cm < n && kfa[e] == kk[e + 1];
+            const bool tail = ok && (ie + 1 == nr || kk[e + 2] != kk[e + 1]);
+            const bool longer = ok && ie + cm < nr && kfa[e] == kk[e + 1];
             hd[e] = head;
             nh += head ? 1 : 0;
             nc += (head && !tail && !longer) ? 1 : 0;
             nhot += (head && longer) ? 1 : 0;
             if (ok) single[vv[e]] = (head && tail) ? 1 : 0;
         }
-        if (pvec && i + 3 < n)
+        if (pvec && i + 3 < nr)
             *(int4*)(perm + i) = v4;
         else
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if (i + e < n) perm[i + e] = vv[e];
+                if (i + e < nr) perm[i + e] = vv[e];
         // (three 10-bit fields: <= 256 per tile)
         const int packed = nh | (nc << 10) | (nhot << 20);
         const int incl = wave_incl_scan(packed), tot = lane63(incl);
         int at = U + ((incl - packed) & 1023);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-            if (hd[e]) R[at++] = i + e;
+            if (hd[e]) R[at++] = nh0 + i + e;
         U += tot & 1023;
         C += (tot >> 10) & 1023;
         H += tot >> 20;
@@ -1165,7 +1172,7 @@ __device__ __forceinline__ void wave_sort_part(const IndexerDev& ix, int v, int 
     WPH(9);
     // segments: the first two tiles keep their flat records in registers for after the reservation
     // returns; later tiles (U > 128) are recomputed then
-    SegPass sp{ix, v, vs, part, n, U, Ks, Vs, R, off, soff};
+    SegPass sp{ix, v, vs, part, n, U, Ks, Vs, R, off, soff, nh0, hkey};
     int c = 0, h = 0, sl0 = 0;
     const SegRec r0 = sp.tile(0, c, h, sl0, true);
     const SegRec r1 = U > 64 ? sp.tile(64, c, h, sl0, true) : SegRec{};

@@ -616,29 +616,34 @@ static void launch_step_index(hipStream_t s, const PrepArgs& pa) {
 // p = b L + k) as three short launches, partition first, so no workgroup reads more than its own
 // share of the indices (the scan build reads the whole table once per 4 parts: 64 times at 256
 // parts, 183 us for configs[4]; the hash build it replaces took 146 us with 13x its algorithmic
-// bytes in global atomics):
+// bytes in global atomics).  P = 2^(wave_vshift(N) - 1) parts per table (128 at 20480):
 //   1. count: one workgroup per 2048-position chunk of a table: each valid position's part
-//      (row & (P - 1), P = 2^wave_vshift(N)) counted in LDS; the chunk's P counts -> keys0
-//      [T][chunks][P].  Out-of-range indices raise the bounds flag and are left out.
-//   2. place: the same chunks again; each workgroup sums the count matrix of its table into the
-//      parts' sizes and offsets (the compact layout: part q at the table's positions in parts < q,
-//      kept in counts[v][CNT_OFF] / [kCntN]) and its chunk's base in every part, then writes each
-//      position as (row >> vs, position) to its part in the HBM scratch (wscratch K0 / V0), in
-//      position order: waves take consecutive quarters of the chunk, tiles of 64 in order, lanes
-//      of one part ranked by ballots (match_digit), one cursor per (wave, part) in LDS.
-//   3. sort: the wave build's last step (wave_sort_part), one wave per part, 4 per workgroup: a
-//      part of <= 512 positions is copied into its quarter of the LDS pool and sorted there (in
-//      registers up to 256 keys), a larger one (hot rows) in the HBM scratch; then segments,
-//      once-hit flags and the flat item lists, exactly as every wave build's.
+//      (row & (P - 1)) counted in LDS; the chunk's P counts -> keys0 [T][chunks][P].  Out-of-range
+//      indices raise the bounds flag and are left out.
+//   2. place: the same chunks again; each workgroup sums its table's count matrix into the parts'
+//      sizes and offsets (the compact layout: part q at the table's positions in parts < q) and
+//      its chunk's base in every part, groups the chunk by part in LDS (waves take consecutive
+//      quarters, tiles of 64 in order, the lanes of one part ranked by ballots -- match_digit --
+//      one cursor per (wave, part)), and writes each part's run of (row >> vs, position) pairs to
+//      the HBM scratch (wscratch K0 / V0) in position order.  The chunk-0 workgroup of a table also
+//      lists its groups (4 parts) for the sort launch, those with a part too big for LDS first
+//      (keys1: the group, its parts' sizes and offsets; two global atomics per table).
+//   3. sort: the wave build's last step (wave_sort_part), one wave per part, 4 per workgroup, in
+//      that order: a part of <= 512 positions is copied into its quarter of the LDS pool and sorted
+//      there (in registers up to 256 keys); a larger one is streamed once: its hot row (the mode
+//      of a 64-key sample) straight to perm as one segment, the rest to LDS, sorted and written
+//      behind it (wave_sort_part's hot prefix); the general HBM sort only if the rest overflows.
+//      Then segments, once-hit flags and the flat item lists, exactly as every wave build's.
 constexpr int kBagChunk = 2048;    // positions per count / place workgroup
 constexpr int kBagLdsPart = 512;   // a part sorted in LDS (its quarter of the pool), else in HBM
-constexpr int kCntN = 6;           // counts[v][kCntN]: the part's size from the count matrix
+constexpr int kBagSlot = 12;       // ints per entry of the sort's group order (keys1): g, 4 sizes, 4 offsets
 
 __global__ __launch_bounds__(256) void bag_count_kernel(PrepArgs pa, int nch) {
     __shared__ int hist[kSegPad];
     const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x;
     const int P = 1 << pa.ix.vshift;
     const uint32_t pmask = (uint32_t)P - 1u;
+    if (c == 0 && t == 0 && tid < 2) pa.ix.keys1[tid] = 0u;  // (bag_place's group-order counters)
     for (int q = tid; q < P; q += 256) hist[q] = 0;
     __syncthreads();
     const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
@@ -676,43 +681,87 @@ __global__ __launch_bounds__(256) void bag_place_kernel(PrepArgs pa, int nch) {
     const int lane = tid & 63, w = tid >> 6;
     const int vs = ix.vshift, P = 1 << vs;
     const uint32_t pmask = (uint32_t)P - 1u;
+    // this wave's quarter of the chunk (kept in registers), loaded first: its latency overlaps the
+    // count matrix's
+    const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
+    constexpr int IT = kBagChunk / 256;  // tiles of 64 per wave
+    constexpr uint32_t kBad = 0xffffffffu;
+    const int pw = c * kBagChunk + w * (kBagChunk / kWaveParts);
+    int64_t xl[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const int p = pw + i * 64 + lane;
+        xl[i] = load_index_if(p < pa.N, pa.idx, pa.itype, (int64_t)t * pa.tstride + p) - pa.base;
+    }
     // part q = tid: its size over the table's chunks and the positions of earlier chunks in it
     const int32_t* cg = (const int32_t*)ix.keys0 + (int64_t)t * nch * P;
     int nq = 0, bef = 0, here = 0;
-    if (tid < P)
-        for (int cc = 0; cc < nch; ++cc) {
-            const int k = cg[(int64_t)cc * P + tid];
-            nq += k;
-            bef += cc < c ? k : 0;
-            here = cc == c ? k : here;
+    if (tid < P) {
+        int k[kWaveMaxN / kBagChunk];
+#pragma unroll
+        for (int cc = 0; cc < kWaveMaxN / kBagChunk; ++cc)  // (every load in flight: nch <= 16)
+            k[cc] = cc < nch ? cg[(int64_t)cc * P + tid] : 0;
+#pragma unroll
+        for (int cc = 0; cc < kWaveMaxN / kBagChunk; ++cc) {
+            nq += k[cc];
+            bef += cc < c ? k[cc] : 0;
+            here = cc == c ? k[cc] : here;
         }
+    }
     int total;
     const int toff = block_scan_nw<kWaveParts, int>(tid < P ? nq : 0, wtot, &total);
     const int loff = block_scan_nw<kWaveParts, int>(tid < P ? here : 0, wtot, &total);
     if (tid < P) {
         cb[tid] = toff + bef;
         cl[tid] = loff;
-        if (c == 0) {
-            int32_t* cn = ix.counts + ((int64_t)(t << vs) + tid) * 8;
-            cn[CNT_OFF] = toff;
-            cn[kCntN] = nq;
-        }
     }
     for (int q = tid; q < kWaveParts * kSegPad; q += 256) (&cw[0][0])[q] = 0;
     __syncthreads();
-    // pass 1: this wave's positions per part (its quarter of the chunk, kept in registers)
-    const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
-    constexpr int IT = kBagChunk / 256;  // tiles of 64 per wave
-    constexpr uint32_t kBad = 0xffffffffu;
-    const int pw = c * kBagChunk + w * (kBagChunk / kWaveParts);
+    if (c == 0) {
+        // the sort launch's order of this table's groups (4 parts each): those holding a part sorted
+        // in HBM (a hot row: its wave's chain is several times a normal part's) go to the front of
+        // keys1[2 ..], the others to the back, so the long chains start first
+        // (two global atomics per table reserve its ranges; ranks within the table by a block scan).
+        // A slot's entry (kBagSlot ints) carries the group and its parts' sizes and offsets, so the
+        // sort's workgroup finds its parts with one load.
+        if (tid < P) {
+            cw[0][tid] = nq > kBagLdsPart ? 1 : 0;
+            cw[2][tid] = nq;
+            cw[3][tid] = toff;
+        }
+        __syncthreads();
+        const int G4 = P / kWaveParts;
+        bool hot = false;
+        if (tid < G4) {
+            const int* f = &cw[0][kWaveParts * tid];
+            hot = (f[0] | f[1] | f[2] | f[3]) != 0;
+        }
+        int nhot;
+        const int hrank = block_scan_nw<kWaveParts, int>(hot ? 1 : 0, wtot, &nhot);
+        if (tid == 0) {
+            cw[1][0] = (int)atomicAdd(&ix.keys1[0], (unsigned)nhot);
+            cw[1][1] = (int)atomicAdd(&ix.keys1[1], (unsigned)(G4 - nhot));
+        }
+        __syncthreads();
+        if (tid < G4) {
+            const int groups = (pa.T << vs) / kWaveParts, g = (t << vs) / kWaveParts + tid;
+            const int at = hot ? cw[1][0] + hrank : groups - 1 - (cw[1][1] + (tid - hrank));
+            uint4* e = (uint4*)(ix.keys1 + kBagSlot * (1 + at));
+            const int q = kWaveParts * tid;
+            e[0] = make_uint4((unsigned)g, 0u, 0u, 0u);
+            e[1] = make_uint4(cw[2][q], cw[2][q + 1], cw[2][q + 2], cw[2][q + 3]);
+            e[2] = make_uint4(cw[3][q], cw[3][q + 1], cw[3][q + 2], cw[3][q + 3]);
+        }
+        __syncthreads();
+        if (tid < P) cw[0][tid] = cw[2][tid] = cw[3][tid] = 0;
+        if (tid < 2) cw[1][tid] = 0;
+        __syncthreads();
+    }
+    // pass 1: this wave's positions per part
     uint32_t xr[IT];
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-        const int p = pw + i * 64 + lane;
-        const bool in = p < pa.N;
-        const int64_t x = load_index_if(in, pa.idx, pa.itype, (int64_t)t * pa.tstride + p) - pa.base;
-        xr[i] = in && (uint64_t)x < nrows ? (uint32_t)x : kBad;
-    }
+    for (int i = 0; i < IT; ++i)
+        xr[i] = pw + i * 64 + lane < pa.N && (uint64_t)xl[i] < nrows ? (uint32_t)xl[i] : kBad;
 #pragma unroll
     for (int i = 0; i < IT; ++i)
         if (xr[i] != kBad) atomicAdd(&cw[w][xr[i] & pmask], 1);
@@ -760,13 +809,19 @@ __global__ __launch_bounds__(256) void bag_sort_kernel(PrepArgs pa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     WaveBuildLds& sl = *(WaveBuildLds*)lds;
     const IndexerDev& ix = pa.ix;
+    // (launch slot -> group: the groups with a part sorted in HBM first; the flat lists' sub-list
+    // is the launch slot's, so every sub-list still takes its fixed share of the waves)
     const int g = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint4* e = (const uint4*)(ix.keys1 + kBagSlot * (1 + g));
+    const uint4 e0 = e[0], e1 = e[1], e2 = e[2];
+    const int gg = (int)e0.x;
     const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;
-    const int t = g / gpt, q0 = (g - t * gpt) * kWaveParts;
+    const int t = gg / gpt, q0 = (gg - t * gpt) * kWaveParts;
     const int v = (t << vs) + q0 + w;
     const int groups = (pa.T << vs) / kWaveParts;
     const uint32_t nrows = (uint32_t)load_table(pa.tabs, t).nrows;
-    const int n = ix.counts[(int64_t)v * 8 + kCntN], toff = ix.counts[(int64_t)v * 8 + CNT_OFF];
+    const int n = (int)(w == 0 ? e1.x : w == 1 ? e1.y : w == 2 ? e1.z : e1.w);
+    const int toff = (int)(w == 0 ? e2.x : w == 1 ? e2.y : w == 2 ? e2.z : e2.w);
     const int64_t S = ix.wstride, o = (int64_t)t * ix.cap + toff;
     uint32_t* K0 = ix.wscratch + o;
     int32_t* V0 = (int32_t*)ix.wscratch + S + o;
@@ -776,10 +831,20 @@ __global__ __launch_bounds__(256) void bag_sort_kernel(PrepArgs pa) {
         const int pb = w * (kBagLdsPart + 4);  // (16-B aligned quarters of the pool)
         uint32_t* LK0 = sl.K[0] + pb;
         int32_t* LV0 = sl.V[0] + pb;
-        for (int i = lane; i < n; i += 64) {
-            LK0[i] = K0[i];
-            LV0[i] = V0[i];
+        uint32_t kk[kBagLdsPart / 64];
+        int32_t vv[kBagLdsPart / 64];
+#pragma unroll
+        for (int j = 0; j < kBagLdsPart / 64; ++j) {  // (every load in flight)
+            const int i = 64 * j + lane;
+            kk[j] = i < n ? K0[i] : 0u;
+            vv[j] = i < n ? V0[i] : 0;
         }
+#pragma unroll
+        for (int j = 0; j < kBagLdsPart / 64; ++j)
+            if (64 * j + lane < n) {
+                LK0[64 * j + lane] = kk[j];
+                LV0[64 * j + lane] = vv[j];
+            }
         wave_lds_sync();
         if (n > kRegSortMax && nbits > 0 && bag_hot_sort<false>(n, nbits, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb))
             wave_sort_part<false, false, true>(ix, v, t, vs, nrows, n, toff, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb,
@@ -788,13 +853,64 @@ __global__ __launch_bounds__(256) void bag_sort_kernel(PrepArgs pa) {
             wave_sort_part<false>(ix, v, t, vs, nrows, n, toff, LK0, LV0, sl.K[1] + pb, sl.V[1] + pb, sl.R + pb,
                                   sl.cnt[w], g, groups);
     } else {
-        uint32_t* K1 = ix.wscratch + 2 * S + o;
-        int32_t* V1 = (int32_t*)ix.wscratch + 3 * S + o;
-        int32_t* R = (int32_t*)ix.wscratch + 4 * S + o;
-        if (nbits > 0 && bag_hot_sort<true>(n, nbits, K0, V0, K1, V1))
-            wave_sort_part<true, false, true>(ix, v, t, vs, nrows, n, toff, K0, V0, K1, V1, R, sl.cnt[w], g, groups);
-        else
+        // A part too big for LDS is nearly always one hot row plus a few hundred others (Zipf rows).
+        // The wave streams it once, 512 entries per round trip: the most frequent key of a 64-key
+        // sample is taken as the hot row, its positions go straight to perm (one segment, in position
+        // order, once-hit flags 0), the others to its LDS quarter; those are then sorted and written
+        // as a part with a hot prefix.  If the others overflow the quarter, or the row is not hot
+        // after all, the part is sorted in HBM the general way (which rewrites perm and the flags).
+        const int pb = w * (kBagLdsPart + 4);
+        uint32_t* LK1 = sl.K[1] + pb;
+        int32_t* LV1 = sl.V[1] + pb;
+        const uint32_t mine = K0[(int64_t)lane * n / 64];
+        int cmode = 0;
+        for (int j = 0; j < 64; ++j) cmode += __shfl(mine, j, 64) == mine ? 1 : 0;
+        int best = (cmode << 6) | lane;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) best = max(best, __shfl_xor(best, d, 64));
+        const uint32_t hkey = __shfl(mine, best & 63, 64);
+        int32_t* perm = ix.perm + o;
+        uint8_t* single = ix.single + (int64_t)t * ix.cap;
+        const unsigned long long below = lanes_below();
+        int hrun = 0, rrun = 0;
+        for (int c0 = 0; c0 < n; c0 += kBagLdsPart) {
+            uint32_t kk[kBagLdsPart / 64];
+            int32_t vv[kBagLdsPart / 64];
+#pragma unroll
+            for (int j = 0; j < kBagLdsPart / 64; ++j) {  // (every load of the round in flight)
+                const int i = c0 + 64 * j + lane;
+                kk[j] = i < n ? K0[i] : ~hkey;
+                vv[j] = i < n ? V0[i] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kBagLdsPart / 64; ++j) {
+                const bool ok = c0 + 64 * j + lane < n;
+                const bool hot = ok && kk[j] == hkey;
+                const unsigned long long hb = __ballot(hot), rb = __ballot(ok && !hot);
+                if (hot) {
+                    perm[hrun + __popcll(hb & below)] = vv[j];
+                    single[vv[j]] = 0;
+                } else if (ok) {
+                    const int at = rrun + __popcll(rb & below);
+                    if (at < kBagLdsPart) {
+                        LK1[at] = kk[j];
+                        LV1[at] = vv[j];
+                    }
+                }
+                hrun += __popcll(hb);
+                rrun += __popcll(rb);
+            }
+        }
+        if (rrun <= kBagLdsPart && hrun > kChunk && nbits > 0) {
+            wave_lds_sync();
+            wave_sort_part<false>(ix, v, t, vs, nrows, n, toff, LK1, LV1, sl.K[0] + pb, sl.V[0] + pb, sl.R + pb,
+                                  sl.cnt[w], g, groups, hrun, hkey);
+        } else {
+            uint32_t* K1 = ix.wscratch + 2 * S + o;
+            int32_t* V1 = (int32_t*)ix.wscratch + 3 * S + o;
+            int32_t* R = (int32_t*)ix.wscratch + 4 * S + o;
             wave_sort_part<true>(ix, v, t, vs, nrows, n, toff, K0, V0, K1, V1, R, sl.cnt[w], g, groups);
+        }
     }
 }
 static_assert(kWaveParts * (kBagLdsPart + 4) <= kStepIndexMaxN + 16, "bag sort: four quarters of the pool");
@@ -803,7 +919,8 @@ int launch_bag_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs,
                      int64_t tstride, int base, int N, unsigned* err) {
     if (T_ == 0 || N == 0) return DLRM_OK;
     const int nch = (N + kBagChunk - 1) / kBagChunk;
-    if (ix.vshift < 2 || ix.vshift > kWaveMaxVshift || ix.wstride <= 0 || (int64_t)nch * (1 << ix.vshift) > ix.cap)
+    if (ix.vshift < 2 || ix.vshift > kWaveMaxVshift || ix.wstride <= 0 || (int64_t)nch * (1 << ix.vshift) > ix.cap ||
+        (int64_t)kBagSlot * ((T_ << ix.vshift) / kWaveParts + 1) > (int64_t)T_ * ix.cap)
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "bag build: N %d, vshift %d, capacity %lld", N, ix.vshift,
                         (long long)ix.cap);
     const PrepArgs pa{ix, tabs, T_, idx, itype, tstride, base, N, err};

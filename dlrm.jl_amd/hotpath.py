@@ -88,7 +88,8 @@ class HotPath:
         mode = {False: None, 0: None, None: None, True: "side", 1: "side", 2: "apply"}.get(pipeline, pipeline)
         if mode not in (None, "side", "apply"):
             raise ValueError(f"pipeline must be None, 'side' or 'apply', not {pipeline!r}")
-        self.pipeline = mode if (mode and self.step_api and self.L == 1) else None
+        # (pooled bags: "side" only -- the next batch's build beside this step's apply, `step_next`)
+        self.pipeline = mode if (mode and ((self.step_api and self.L == 1) or (mode == "side" and self.L > 1))) else None
         self._prepare_ok = None  # build_split: None untried, False the wave build does not take it
         if self.pipeline:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
@@ -215,7 +216,12 @@ class HotPath:
             self._cur, self._ix_of = 1, [None, None]
             self.step_prep(x, prev, dout, idx)
             return
-        self.build_split(self._ixs[self._cur], idx)
+        if self.L > 1:  # pooled bags: dlrm_indexer_build (the bag build)
+            home, self.indexer = self.indexer, self._ixs[self._cur]
+            self.build_indexer(idx)
+            self.indexer = home
+        else:
+            self.build_split(self._ixs[self._cur], idx)
         self._ix_of[self._cur] = idx
 
     def step_prep(self, x, idx, dout, next_idx):
@@ -240,6 +246,8 @@ class HotPath:
         if self._ix_of[cur] is not idx:  # out of sequence (first call, or a different batch)
             self.prime(idx)
         main = torch.cuda.current_stream(self.ts.device)
+        if self.L > 1:
+            return self._step_bags_next(main, x, idx, dout, next_idx, cur, nxt)
         self._pside.wait_stream(main)
         with torch.cuda.stream(self._pside):
             self.build_split(self._ixs[nxt], next_idx)
@@ -248,6 +256,33 @@ class HotPath:
         self.lookup_interact_fwd(x, idx)  # ys not materialized: the fused forward alone
         self.indexer = self._ixs[cur]
         self.step_bwd(dout, x=x, idx=idx)
+        main.wait_event(self._pev)
+        self._cur = nxt
+        return self.dx
+
+    def _step_bags_next(self, main, x, idx, dout, next_idx, cur, nxt):
+        """step_next for pooled bags (configs[4]): forward and backward on the main stream, then the
+        apply of batch `idx` with its prebuilt indexer while batch `next_idx`'s bag build runs on the
+        side stream beside it, forked when the backward is queued and joined at the end of the step.
+        The apply (hundreds of us of latency-bound items) hides the build; beside the gather-heavy
+        forward (the unpipelined form) the build's kernels and the forward's slowed each other and
+        the step paid the build's length."""
+        if self.fused:  # (not self.forward: that forks this batch's own build)
+            self.lookup_interact_fwd(x, idx)
+        else:
+            self.lookup(idx)
+            self.interact_fwd(x)
+        self.interact_bwd(dout, x=x, idx=idx)
+        self._pside.wait_stream(main)  # (also: the apply that last read indexer nxt is done)
+        with torch.cuda.stream(self._pside):
+            home, self.indexer = self.indexer, self._ixs[nxt]
+            self.build_indexer(next_idx)
+            self.indexer = home
+            self._pev.record(self._pside)
+        self._ix_of[nxt] = next_idx
+        home, self.indexer = self.indexer, self._ixs[cur]
+        self.sgd_update(idx, True)
+        self.indexer = home
         main.wait_event(self._pev)
         self._cur = nxt
         return self.dx

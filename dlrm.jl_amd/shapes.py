@@ -59,9 +59,12 @@ def step_pipeline(w):
     config 49.1M vs 43.8M samples/s with the build in the forward's launch), "side" = the next
     batch's build on a side stream (one-hot batches > 2048: the in-LDS parts build; the in-apply wave
     build takes up to 16384 positions per table but measured slower at 8192, APPLY_MAX_N), None =
-    inside the forward's launch (pooled bags: the operator path, which builds its own)."""
+    pooled bags: the operator path, whose bag build runs on a side stream beside the forward.  (The
+    pooled "side" form -- the next batch's bag build beside this step's apply, HotPath.step_next --
+    measured the same, 674.6 vs 670 us per step: the stages' sum either way, as the forward and the
+    persistent apply fill every CU slot; round 6.)"""
     L, B = w["lookups"], w["batch"]
-    if L != 1:
+    if L != 1:  # pooled bags: the operator path (its bag build on a side stream beside the forward)
         return None
     return "apply" if B <= APPLY_MAX_N else "side"
 

@@ -178,15 +178,22 @@ def test_kaggle_bf16_b8192_step_vs_oracle(pkg, gpu):
 def test_pooled_64x256_l10_zipf_step_vs_oracle(pkg, gpu):
     """configs[4] at 100k rows per table (the oracle's size): 64 tables x 256 fp32, L = 10 sum-pooled
     bags, Zipf(1.2) hot rows, B = 2048 -- the bench's pooled path (many-wave pooled gather, the
-    interaction at d = 256 / F = 65, hash indexer, the hot-segment apply) against the oracle."""
+    interaction at d = 256 / F = 65, the bag build on a side stream, the hot-segment apply) over two
+    consecutive batches, against the oracle; and the pipelined form (the next batch's bag build
+    beside the apply, HotPath.step_next) the same way."""
     rows = [100_000] * 64
     D, B, L = 256, 2048, 10
     g = torch.Generator(device=gpu).manual_seed(21)
     tables = [torch.empty((n, D), device=gpu).uniform_(-n ** -0.5, n ** -0.5, generator=g) for n in rows]
     rng = np.random.default_rng(22)
-    idx = zipf_indices(pkg, rng, rows, B * L, 1.2)
-    hp = run_step_vs_oracle(pkg, gpu, tables, idx, B, L, 0.05, torch.float32, seed=23)
-    assert hp.materialize_ys  # pooled bags keep ys (the bench's form)
+    idx = [zipf_indices(pkg, rng, rows, B * L, 1.2) for _ in range(2)]
+    pipeline = pkg.step_pipeline(pkg.WORKLOADS["pooled-64x256-l10"])
+    keep = [t.clone() for t in tables]
+    hp = run_step_vs_oracle(pkg, gpu, tables, idx, B, L, 0.05, torch.float32, seed=23, pipeline=pipeline)
+    assert hp.materialize_ys and pipeline is None  # pooled bags keep ys (the bench's form)
+    del hp
+    hp = run_step_vs_oracle(pkg, gpu, keep, idx, B, L, 0.05, torch.float32, seed=23, pipeline="side")
+    assert hp.pipeline == "side"
 
 
 def test_pooled_full_size_properties(pkg, gpu):

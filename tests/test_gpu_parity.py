@@ -413,18 +413,27 @@ def test_prepared_step_equals_fresh_step_and_bounds(pkg, gpu):
         assert np.array_equal(to_np_f32(hp2.ts[t].data), tabs[t]), f"table {t} was written on a BoundsError step"
 
 
-@pytest.mark.parametrize("rows,B,L,zipf", [
-    ([1_000_000] * 6, 2048, 10, 1.2),          # configs[4]'s bags: 20480 positions per table, Zipf(1.2)
-    ([3, 1000, 40, 5_000_000], 3000, 8, None),  # 24000: tiny tables (one row per part: DIRECT), uniform
-    ([7, 100_000], 4096, 8, 1.05),              # 32768: the largest wave build
-    ([1_000_000] * 2, 1000, 9, 1.2)])           # 9000: N % 256 != 0
-def test_bag_wave_build_segments(pkg, gpu, rows, B, L, zipf):
-    """dlrm_indexer_build of pooled bags with 8192 < B L <= 32768 positions per table: the wave scan
-    build (round 6; it replaced the hash build for configs[4]) groups the positions p = b L + k
-    exactly as numpy does; then a prebuilt update_ (the apply maps p to its bag) equals the
-    closed-form scatter-add of integer bag gradients on every touched row, and writes no other row."""
+@pytest.mark.parametrize("rows,B,L,zipf,case", [
+    ([1_000_000] * 6, 2048, 10, 1.2, ""),          # configs[4]'s bags: 20480 positions per table, Zipf(1.2)
+    ([3, 1000, 40, 5_000_000], 3000, 8, None, ""),  # 24000: tiny tables (one row per part), uniform
+    ([7, 100_000], 4096, 8, 1.05, ""),              # 32768: the largest wave build
+    ([1_000_000] * 2, 1000, 9, 1.2, ""),            # 9000: N % 256 != 0
+    ([1_000_000], 2048, 10, None, "two-hot"),       # two hot rows in one part: the general HBM sort
+    ([1_000_000], 2048, 10, None, "hot+300")])      # a hot row + ~380 others: LDS counting passes
+def test_bag_wave_build_segments(pkg, gpu, rows, B, L, zipf, case):
+    """dlrm_indexer_build of pooled bags with 8192 < B L <= 32768 positions per table: the bag build
+    (round 6: count, place by part, per-part sort, a streamed hot-row prefix for parts too big for
+    LDS; it replaced the hash build for configs[4]) groups the positions p = b L + k exactly as
+    numpy does; then a prebuilt update_ (the apply maps p to its bag) equals the closed-form
+    scatter-add of integer bag gradients on every touched row, and writes no other row."""
     rng = np.random.default_rng(B * L + len(rows))
     idx = rand_indices(rng, rows, B, L, zipf=zipf)
+    if case == "two-hot":  # rows 7 and 7 + 3 * 256: both in part 7 of 256, a third of the positions each
+        idx[0, 0::3] = 7
+        idx[0, 1::3] = 7 + 3 * 256
+    elif case == "hot+300":  # row 9 at a fifth of the positions, 300 more distinct rows of part 9
+        idx[0, 0::5] = 9
+        idx[0, 1:1501:5] = 9 + 256 * rng.choice(np.arange(1, 3900), size=300, replace=False)
     D = 16
     tabs = pkg.EmbeddingTableSet([torch.zeros((n, D), device=gpu) for n in rows])
     ix = pkg.SparseIndexer(len(rows), B * L, gpu)
