@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--chunk", type=int, default=-1,
                     help="the wave build's chunk limit (16 or 32; 0: the library's default 32); -1 (default): "
                          "pkg.step_chunk (16 for uniform one-hot batches, 32 for Zipf rows)")
+    ap.add_argument("--parts", type=int, default=-1,
+                    help="parts per table of the step's wave build (16, 32 or 64; 0: the library's 16); -1 "
+                         "(default): pkg.step_parts (32 for rows <= 256 B)")
     ap.add_argument("--materialize-ys", type=int, default=-1,
                     help="1: forward writes ys and backward reads it (reference data flow); 0: backward "
                          "re-gathers T; -1 (default): 0 where it applies (fused, lookups=1)")
@@ -395,7 +398,8 @@ def main():
                              fused=bool(a.fused),
                              materialize_ys=None if a.materialize_ys < 0 else bool(a.materialize_ys),
                              pipeline={0: None, 1: "side", 2: "apply"}[a.pipeline],
-                             chunk=pkg.step_chunk(w) if a.chunk < 0 else (a.chunk or None))
+                             chunk=pkg.step_chunk(w) if a.chunk < 0 else (a.chunk or None),
+                             parts=pkg.step_parts(w) if a.parts < 0 else (a.parts or None))
         F = T + 1
         dtp = tables[0].dtype
         x = torch.randn((B, D), device=dev, generator=g).to(dtp)
@@ -648,6 +652,8 @@ def main():
         for ix in indexers:
             if engine.chunk:
                 ix.set_chunk(engine.chunk)  # (the engine's chunk limit)
+            if engine.parts:
+                ix.set_parts(engine.parts)
         home = engine.indexer
         for k in range(nb):
             engine.indexer = indexers[k]
@@ -686,6 +692,8 @@ def main():
             for ix in nxt:
                 if engine.chunk:
                     ix.set_chunk(engine.chunk)
+                if engine.parts:
+                    ix.set_parts(engine.parts)
 
             def apply_prep_k(k):
                 engine.indexer = indexers[k]

@@ -17,7 +17,7 @@ from .lazy import DeferredUpdate, HipTables, LazyGrad, LazyLookup
 from .interact import (POST_INTERACTION_PAD_TO_MUL, DotInteraction, cdiv, dot_back, dot_interaction, fast_vcat,
                        interaction_sizes, rrule, rrule_dot_interaction, rrule_self_batched_mul, rrule_triangular_slice,
                        self_batched_mul, triangular_slice, triangular_slice_back, up_to_mul_of)
-from .shapes import (KAGGLE_EMBEDDING_SIZES, TERABYTE_EMBEDDING_SIZES, WORKLOADS, step_chunk, step_pipeline, zipf_perm,
+from .shapes import (KAGGLE_EMBEDDING_SIZES, TERABYTE_EMBEDDING_SIZES, WORKLOADS, step_chunk, step_parts, step_pipeline, zipf_perm,
                      zipf_rows)
 from .update import Descent, SparseEmbeddingUpdate, SparseIndexer, maplookup_pullback, update_
 
@@ -29,6 +29,6 @@ __all__ = [
     "SparseIndexer", "maplookup_pullback", "update_", "DenseMLP", "DLRMModel", "bce_loss", "bce_loss_back",
     "kaggle_mlp_sizes", "random_mlp", "dac", "DAC_DTYPE", "DACLoader", "DACMaps", "ShardedDLRMModel",
     "dot_interaction", "rrule_dot_interaction", "triangular_slice", "triangular_slice_back", "rrule_triangular_slice",
-    "self_batched_mul", "rrule_self_batched_mul", "step_pipeline", "step_chunk", "zipf_perm", "HipTables", "LazyLookup",
+    "self_batched_mul", "rrule_self_batched_mul", "step_pipeline", "step_chunk", "step_parts", "zipf_perm", "HipTables", "LazyLookup",
     "LazyGrad", "DeferredUpdate",
 ]

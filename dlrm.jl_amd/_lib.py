@@ -89,6 +89,7 @@ SIGNATURES = {
     "dlrm_indexer_bytes": (_i32, [_vp, _vp]),
     "dlrm_indexer_reserve": (_i32, [_vp, _vp, _i32]),
     "dlrm_indexer_set_chunk": (_i32, [_vp, _vp, _i32]),
+    "dlrm_indexer_set_parts": (_i32, [_vp, _vp, _i32]),
     "dlrm_sgd_update": (_i32, [_vp, _vp, _vp, _u32, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64, _i64, _f32]),
     "dlrm_bce_head": (_i32, [_vp, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "dlrm_relu_bwd_bias_workspace": (_i32, [_i32, _i32, _pi64, _pi64]),

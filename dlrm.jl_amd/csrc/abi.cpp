@@ -48,6 +48,7 @@ struct dlrm_tables {
 struct dlrm_indexer {
     dlrm_ctx* ctx = nullptr;
     int T = 0;
+    int parts_log2 = 0;  // the wave builds of <= 2048 positions per table: log2 parts (0: the default, 16)
     int TV = 0;  // tables of the per-table arrays: 4T when the forward launch may split tables by row bits
     IndexerDev dev{};
     void* block = nullptr;  // one allocation for every array
@@ -123,8 +124,9 @@ static int step_parts_log2(int dflt = kStepParts) {
 // vshift of the wave build of `batch` positions per table (the step forward's in-launch build and
 // the in-apply / prepared builds): 16 parts per table up to 2048 positions (DLRM_STEP_PARTS may force
 // fewer, >= 4), then 16 parts per 2048 positions (wave_vshift)
-static int wave_parts_log2(int64_t batch) {
+static int wave_parts_log2(int64_t batch, const dlrm_indexer* ix = nullptr) {
     if (batch > kStepIndexMaxN) return wave_vshift(batch);
+    if (ix && ix->parts_log2 && !knobs().step_parts) return ix->parts_log2;  // (dlrm_indexer_set_parts)
     const int vs = step_parts_log2(kWaveBuildParts);
     return vs < 2 ? 2 : vs;
 }
@@ -611,9 +613,9 @@ static int indexer_carve(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
     const int64_t T0 = ix->T > 0 ? ix->T : 1;
     const int64_t T = (int64_t)parts * T0;
     const int64_t hs = ix->dev.hsize;
-    // the largest wave build this indexer takes: 2^vw parts per table, T0 << vw / 4 workgroups (>= 32
-    // parts: the builds of <= 2048 positions may take 32, DLRM_STEP_PARTS)
-    const int vw = std::max(wave_vshift(cap < kWaveMaxN ? cap : kWaveMaxN), 5);
+    // the largest wave build this indexer takes: 2^vw parts per table, T0 << vw / 4 workgroups (>= 64
+    // parts: the builds of <= 2048 positions may take 32 or 64, dlrm_indexer_set_parts)
+    const int vw = std::max(wave_vshift(cap < kWaveMaxN ? cap : kWaveMaxN), 6);
     const int64_t TW = T0 << vw;
     // carve every array out of one allocation (16-B aligned pieces)
     struct Piece { void** p; size_t bytes; };
@@ -719,6 +721,14 @@ int dlrm_indexer_set_chunk(dlrm_ctx* ctx, dlrm_indexer* ix, int max_positions) {
     return DLRM_OK;
 }
 
+int dlrm_indexer_set_parts(dlrm_ctx* ctx, dlrm_indexer* ix, int parts) {
+    CHECK_ARG(ctx && ix, "dlrm_indexer_set_parts: null argument");
+    CHECK_ARG(parts == 0 || parts == 16 || parts == 32 || parts == 64, "dlrm_indexer_set_parts: %d (0, 16, 32 or 64)",
+              parts);
+    ix->parts_log2 = parts == 64 ? 6 : (parts == 32 ? 5 : (parts == 16 ? 4 : 0));
+    return DLRM_OK;
+}
+
 int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* ix, int batch) {
     CHECK_ARG(ctx && ix, "dlrm_indexer_reserve: null argument");
     CHECK_ARG(batch >= 0 && batch <= ix->dev.cap, "dlrm_indexer_reserve: batch %d > capacity %lld", batch,
@@ -812,7 +822,7 @@ int dlrm_indexer_prepare(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables* tb,
     if (rc) return rc;
     CHECK_ARG(tb->T == ix->T, "dlrm_indexer_prepare: indexer has %d tables, tables has %d", ix->T, tb->T);
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_prepare: batch %d > capacity %lld", batch, (long long)ix->dev.cap);
-    const int vs = wave_parts_log2(batch);
+    const int vs = wave_parts_log2(batch, ix);
     if (!wave_fits(ix, batch))
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "dlrm_indexer_prepare: batch %d (the wave build: batch <= %d, "
                         "tables x capacity < 2^31)", batch, kWaveMaxN);
@@ -983,7 +993,7 @@ int dlrm_step_fwd(dlrm_ctx* ctx, const dlrm_tables* tb, dlrm_indexer* ix, const 
     ix->prepared = false;
     ix->built = false;
     // the wave build in the forward's launch (vshift >= 2: it also writes the apply's item map)
-    ix->dev.vshift = ix->dev.cap <= kWaveApplyMaxN && wave_fits(ix, batch) ? wave_parts_log2(kStepIndexMaxN) : 0;
+    ix->dev.vshift = ix->dev.cap <= kWaveApplyMaxN && wave_fits(ix, batch) ? wave_parts_log2(kStepIndexMaxN, ix) : 0;
     rc = launch_step_fwd(ctx, tb->d_desc, tb->aligned16, tb->T, tb->dtype, indices, itype, table_stride, index_base, d,
                          batch, x, x_ld, out, out_ld, padding, ix->dev, tb->h_desc.data());
     if (rc == DLRM_OK) {
@@ -1128,7 +1138,7 @@ int dlrm_step_bwd_prepare(dlrm_ctx* ctx, dlrm_tables* tb, dlrm_indexer* ix, cons
     next->built = false;
     next->prepared = false;
     // the wave build: 2^wave_parts_log2(batch) parts per table, one wave each (4 per workgroup)
-    next->dev.vshift = wave_parts_log2(batch);
+    next->dev.vshift = wave_parts_log2(batch, next);
     if (next->dev.vshift < 2) next->dev.vshift = 2;
     const PrepArgs pa{next->dev, tb->d_desc, tb->T, next_indices, itype, table_stride, index_base, batch,
                       next->prep_err + 1};

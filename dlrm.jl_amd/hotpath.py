@@ -37,7 +37,8 @@ from .update import SparseIndexer
 
 class HotPath:
     def __init__(self, tables, batch, lookups=1, *, lr=0.1, index_base=0, deterministic=True,
-                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None, pipeline=False, chunk=None):
+                 overlap_indexer=None, pad_to=1, fused=True, materialize_ys=None, pipeline=False, chunk=None,
+                 parts=None):
         self.ts = tables if isinstance(tables, EmbeddingTableSet) else EmbeddingTableSet(tables)
         self.B, self.L = int(batch), int(lookups)
         self.T, self.D = len(self.ts), self.ts.D
@@ -65,6 +66,11 @@ class HotPath:
         self.chunk = chunk
         if chunk is not None and self.indexer is not None:
             self.indexer.set_chunk(chunk)
+        # parts per table of the wave builds of <= 2048 positions (None: the library's 16;
+        # shapes.step_parts picks per workload)
+        self.parts = parts
+        if parts is not None and self.indexer is not None:
+            self.indexer.set_parts(parts)
         self.ctx = self.ts.ctx
         self.lib = self.ctx.lib
         self.dcode = dtype_code(dt)
@@ -95,6 +101,8 @@ class HotPath:
             self._ixs = [self.indexer, SparseIndexer(self.T, self.B * self.L, dev)]
             if chunk is not None:
                 self._ixs[1].set_chunk(chunk)
+            if parts is not None:
+                self._ixs[1].set_parts(parts)
             if self.pipeline == "apply" and self.B > 2048:  # (the in-apply wave build's parts, before any capture)
                 for ix in self._ixs:
                     ix.reserve(self.B)

@@ -359,6 +359,10 @@ reserve!(ix::HipIndexer, batch::Integer) =
 set_chunk!(ix::HipIndexer, max_positions::Integer) =
     check(ix.ctx, ccall((:dlrm_indexer_set_chunk, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), ix.ctx.ptr, ix.ptr,
                         max_positions))
+"Parts per table of the indexer's later wave builds of <= 2048 positions (0 = 16, 32 or 64; same segments)."
+set_parts!(ix::HipIndexer, parts::Integer) =
+    check(ix.ctx, ccall((:dlrm_indexer_set_parts, libdlrm), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), ix.ctx.ptr, ix.ptr,
+                        parts))
 "Device bytes the indexer holds."
 function nbytes(ix::HipIndexer)
     b = Ref{Int64}(0)

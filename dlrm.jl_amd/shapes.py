@@ -81,6 +81,18 @@ def step_chunk(w):
     return 16
 
 
+def step_parts(w):
+    """Parts per table of the step's wave build for workload `w` (HotPath(parts=...),
+    dlrm_indexer_set_parts): 32 where a row is <= 256 B -- the apply's items are light and the next
+    batch's build is the apply launch's long pole, so shortening its chain (half the positions per
+    wave) wins: D = 16 80.8 -> 85.5 M samples/s, Terabyte bf16 rows 52.0 -> 57.7 M (apply 17.5 ->
+    11.8 us) -- and the library's 16 at 512-B rows, where the extra build workgroups cost the heavier
+    apply more (metric 56.8 -> 55.0 M with 32); round 6, profiles/r15/parts_ab."""
+    if w["lookups"] != 1:
+        return None
+    return 32 if w["dim"] * (2 if w["dtype"] == "bf16" else 4) <= 256 else None
+
+
 def table_bytes(rows, dim, esize):
     return sum(rows) * dim * esize
 

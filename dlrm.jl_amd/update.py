@@ -140,6 +140,12 @@ class SparseIndexer:
         self.ctx.check(self.ctx.lib.dlrm_indexer_set_chunk(self.ctx.bind(), self.handle, int(max_positions)))
         return self
 
+    def set_parts(self, parts):
+        """Parts per table of later wave builds of <= 2048 positions (0 / 16, 32 or 64;
+        dlrm_indexer_set_parts): the same segments whatever the setting."""
+        self.ctx.check(self.ctx.lib.dlrm_indexer_set_parts(self.ctx.bind(), self.handle, int(parts)))
+        return self
+
     def nbytes(self):
         """Device bytes held (dlrm_indexer_bytes: all allocated at creation, never grown)."""
         b = ctypes.c_int64()

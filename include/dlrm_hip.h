@@ -271,6 +271,12 @@ int dlrm_indexer_reserve(dlrm_ctx* ctx, dlrm_indexer* indexer, int batch);
  * 105-row Kaggle table) into one-round items (DESIGN.md §3 "Round 6").  Deterministic either way; a
  * 17..32-position segment is summed in a different (fixed) order, so its fp32 rounding may differ. */
 int dlrm_indexer_set_chunk(dlrm_ctx* ctx, dlrm_indexer* indexer, int max_positions);
+/* Parts per table of this indexer's later wave builds of <= 2048 positions per table (the step's
+ * in-apply / forward-launch builds, dlrm_indexer_prepare): 16 (the default, 0), 32 or 64; one wave
+ * sorts each part.  More parts shorten the build's chain and add workgroups beside the apply: a
+ * win where the apply's items are light (rows <= 256 B: D = 16 fp32, Terabyte bf16 rows), a loss
+ * at 512-B rows (DESIGN.md §3 "Round 6").  Results are identical for any setting. */
+int dlrm_indexer_set_parts(dlrm_ctx* ctx, dlrm_indexer* indexer, int parts);
 
 /* Host-side state of the last build (no GPU call): a mask of DLRM_IX_* bits.  SINGLES_DONE: a
  * split backward (dlrm_step_bwd) has stepped this build's once-hit rows, so its dt holds only

@@ -154,8 +154,8 @@ def test_bench_form_vs_oracle(pkg, gpu, workload):
     batches = [np.stack([rng.integers(0, n, size=B) for n in w["rows"]]).astype(np.int64) for _ in range(2)]
     pipeline = pkg.step_pipeline(w)
     hp = run_step_vs_oracle(pkg, gpu, tables, batches, B, 1, 0.05, dtype, seed=B, pipeline=pipeline,
-                            hot_kw={"chunk": pkg.step_chunk(w)})
-    assert hp.step_api and hp.chunk == pkg.step_chunk(w)
+                            hot_kw={"chunk": pkg.step_chunk(w), "parts": pkg.step_parts(w)})
+    assert hp.step_api and hp.chunk == pkg.step_chunk(w) and hp.parts == pkg.step_parts(w)
 
 
 # ---------------------------------------------------------------------------- configs[2]
@@ -274,8 +274,10 @@ def test_terabyte_bf16_full_size(pkg, gpu):
         tab[u] = torch.empty((len(u), D), device=gpu).uniform_(-0.05, 0.05, generator=g).to(torch.bfloat16)
     pipeline = pkg.step_pipeline(pkg.WORKLOADS["terabyte-d128-bf16-zipf"])
     assert pipeline == "apply"
+    w = pkg.WORKLOADS["terabyte-d128-bf16-zipf"]
     hp = run_step_vs_oracle(pkg, gpu, tables, [idx_np, idx2_np], B, 1, 0.05, torch.bfloat16, seed=43,
-                            pipeline=pipeline)
+                            pipeline=pipeline, hot_kw={"chunk": pkg.step_chunk(w), "parts": pkg.step_parts(w)})
+    assert hp.parts == 32  # (the bench's form: 256-B rows)
     del hp
     # (3) exact integer-gradient update on zeroed tables
     for tab in tables:

@@ -298,6 +298,11 @@ def test_wave_prepare_segments(pkg, gpu, rows, B, zipf, case):
     assert ix.prepare(tabs, torch.from_numpy(idx).to(itype).to(gpu), index_base=0)
     tabs.ctx.check_bounds()
     _assert_segments(ix, idx, B)
+    if B <= 2048:  # the same segments with 32 and 64 parts per table (dlrm_indexer_set_parts)
+        for parts in (32, 64):
+            ix.set_parts(parts)
+            assert ix.prepare(tabs, torch.from_numpy(idx).to(itype).to(gpu), index_base=0)
+            _assert_segments(ix, idx, B)
 
 
 @pytest.mark.parametrize("rows,B,table,where,value,itype,zipf", [
@@ -1383,22 +1388,25 @@ def test_exchange_layout_kernels(pkg, gpu, dtype):
 
 
 @pytest.mark.parametrize("mode", ["side", "apply"])
-@pytest.mark.parametrize("rows,D,B,dtype", [("kaggle", 128, 2048, torch.float32),
-                                            ("kaggle", 16, 2048, torch.float32),
-                                            ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32),
-                                            # configs[2]'s shape: the in-apply wave build at 8192
-                                            ("kaggle", 128, 8192, torch.bfloat16),
-                                            ([3, 500, 100000, 2_000_000], 32, 16384, torch.float32),
-                                            ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16),
-                                            # Terabyte-shaped bf16 x 128 at B = 2048: the in-apply
-                                            # build runs 8 parts per table (256-B rows)
-                                            ([3, 200000, 60, 50000, 10, 100000] * 4 + [7, 30000], 128, 2048,
-                                             torch.bfloat16)])
-def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype, mode):
+@pytest.mark.parametrize("rows,D,B,dtype,parts", [("kaggle", 128, 2048, torch.float32, None),
+                                                  ("kaggle", 16, 2048, torch.float32, None),
+                                                  ("kaggle", 16, 2048, torch.float32, 32),  # (the bench's D = 16 form)
+                                                  ("kaggle", 128, 2048, torch.float32, 64),
+                                                  ([300, 100000, 3, 5_000_000], 64, 6000, torch.float32, None),
+                                                  # configs[2]'s shape: the in-apply wave build at 8192
+                                                  ("kaggle", 128, 8192, torch.bfloat16, None),
+                                                  ([3, 500, 100000, 2_000_000], 32, 16384, torch.float32, None),
+                                                  ([5, 100000, 3, 77] * 6 + [9, 10], 128, 512, torch.bfloat16, None),
+                                                  # Terabyte-shaped bf16 x 128 at B = 2048 (256-B rows: the
+                                                  # bench builds 32 parts per table)
+                                                  ([3, 200000, 60, 50000, 10, 100000] * 4 + [7, 30000], 128, 2048,
+                                                   torch.bfloat16, 32)])
+def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype, parts, mode):
     """Pipelined steps (the next batch's split indexer built during the step: "side" =
     HotPath.step_next on a side stream, "apply" = HotPath.step_prep inside the apply launch, so
     the next forward only gathers; eager steps, then hipGraph-captured ones) == the operator
-    sequence over the same batches, bit for bit."""
+    sequence over the same batches, bit for bit; also with 32 and 64 parts per table
+    (dlrm_indexer_set_parts: the same segments, so the same bits)."""
     if rows == "kaggle":
         rows = pkg.KAGGLE_EMBEDDING_SIZES
     rng = np.random.default_rng(B + 7)
@@ -1409,7 +1417,8 @@ def test_pipelined_steps_match_operator_sequence(pkg, gpu, rows, D, B, dtype, mo
     x = torch.from_numpy(rng.standard_normal((B, D)).astype(np.float32)).to(gpu).to(dtype)
     F = T + 1
     dout = torch.from_numpy(rng.standard_normal((B, D + F * (F - 1) // 2)).astype(np.float32)).to(gpu).to(dtype)
-    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0, pipeline=mode)
+    hp = pkg.HotPath(pkg.EmbeddingTableSet(dev_tables(tabs, gpu, dtype)), B, 1, lr=0.5, index_base=0, pipeline=mode,
+                     parts=parts)
     assert hp.pipeline == mode
     step = hp.step_next if mode == "side" else hp.step_prep
     order = [0, 1, 2, 0]
