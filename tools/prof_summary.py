@@ -30,7 +30,7 @@ STAGES = [  # (regex on the kernel name, stage)
     (r"interact_fwd_kernel<[^,]+, \d+, false|interact_fwd_scalar", "interact_fwd"),
     (r"interact_bwd", "interact_bwd"),  # incl. interact_bwd_index_kernel
     (r"maplookup_", "lookup"),
-    (r"indexer_build_kernel|indexer_fast_kernel|hix_", "indexer_build"),
+    (r"indexer_build_kernel|indexer_fast_kernel|hix_|bag_(count|place|sort)_kernel|step_index", "indexer_build"),
     (r"sgd_apply|sgd_chunks", "sgd_update"),
     (r"sgd_hot", "sgd_update"),
     (r"sgd_atomic", "sgd_update"),
