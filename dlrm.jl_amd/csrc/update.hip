@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void bag_count_kernel(PrepArgs pa, int nch) {
     const int c = blockIdx.x, t = blockIdx.y, tid = threadIdx.x;
     const int P = 1 << pa.ix.vshift;
     const uint32_t pmask = (uint32_t)P - 1u;
-    if (c == 0 && t == 0 && tid < 2) pa.ix.keys1[tid] = 0u;  // (bag_place's group-order counters)
+    if (c == 0 && t == 0 && tid < 16) pa.ix.keys1[tid] = 0u;  // (bag_place's group-order counters)
     for (int q = tid; q < P; q += 256) hist[q] = 0;
     __syncthreads();
     const uint64_t nrows = (uint64_t)load_table(pa.tabs, t).nrows;
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(256) void bag_place_kernel(PrepArgs pa, int nch) {
     if (c == 0) {
         // the sort launch's order of this table's groups (4 parts each): those holding a part sorted
         // in HBM (a hot row: its wave's chain is several times a normal part's) go to the front of
-        // keys1[2 ..], the others to the back, so the long chains start first
+        // the order list (keys1 from entry 2 on), the others to the back, so the long chains start first
         // (two global atomics per table reserve its ranges; ranks within the table by a block scan).
         // A slot's entry (kBagSlot ints) carries the group and its parts' sizes and offsets, so the
         // sort's workgroup finds its parts with one load.
@@ -738,15 +738,23 @@ __global__ __launch_bounds__(256) void bag_place_kernel(PrepArgs pa, int nch) {
         }
         int nhot;
         const int hrank = block_scan_nw<kWaveParts, int>(hot ? 1 : 0, wtot, &nhot);
+        // Slots by XCD (T % 8 == 0): the tables of eighth j take the slots g = 8 i + j, i.e. the
+        // workgroups on XCD j, whose reservations fill flat sub-list j (indexer.hpp: sub-list = g mod
+        // 8).  The apply splits each item kind into eighths by XCD (pooled bags), so each XCD then
+        // updates an eighth of the tables and reads their bag gradients into its own L2 only.
+        const bool by8 = pa.T % kResLists == 0;
+        const int j8 = by8 ? t / (pa.T / kResLists) : 0;
         if (tid == 0) {
-            cw[1][0] = (int)atomicAdd(&ix.keys1[0], (unsigned)nhot);
-            cw[1][1] = (int)atomicAdd(&ix.keys1[1], (unsigned)(G4 - nhot));
+            cw[1][0] = (int)atomicAdd(&ix.keys1[2 * j8], (unsigned)nhot);
+            cw[1][1] = (int)atomicAdd(&ix.keys1[2 * j8 + 1], (unsigned)(G4 - nhot));
         }
         __syncthreads();
         if (tid < G4) {
             const int groups = (pa.T << vs) / kWaveParts, g = (t << vs) / kWaveParts + tid;
-            const int at = hot ? cw[1][0] + hrank : groups - 1 - (cw[1][1] + (tid - hrank));
-            uint4* e = (uint4*)(ix.keys1 + kBagSlot * (1 + at));
+            const int n8 = by8 ? groups / kResLists : groups;  // (slots of this table's eighth)
+            const int li = hot ? cw[1][0] + hrank : n8 - 1 - (cw[1][1] + (tid - hrank));
+            const int at = by8 ? kResLists * li + j8 : li;
+            uint4* e = (uint4*)(ix.keys1 + kBagSlot * (2 + at));
             const int q = kWaveParts * tid;
             e[0] = make_uint4((unsigned)g, 0u, 0u, 0u);
             e[1] = make_uint4(cw[2][q], cw[2][q + 1], cw[2][q + 2], cw[2][q + 3]);
@@ -812,7 +820,7 @@ __global__ __launch_bounds__(256) void bag_sort_kernel(PrepArgs pa) {
     // (launch slot -> group: the groups with a part sorted in HBM first; the flat lists' sub-list
     // is the launch slot's, so every sub-list still takes its fixed share of the waves)
     const int g = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint4* e = (const uint4*)(ix.keys1 + kBagSlot * (1 + g));
+    const uint4* e = (const uint4*)(ix.keys1 + kBagSlot * (2 + g));
     const uint4 e0 = e[0], e1 = e[1], e2 = e[2];
     const int gg = (int)e0.x;
     const int vs = ix.vshift, gpt = (1 << vs) / kWaveParts;
@@ -920,7 +928,7 @@ int launch_bag_build(dlrm_ctx* ctx, const IndexerDev& ix, const TableDesc* tabs,
     if (T_ == 0 || N == 0) return DLRM_OK;
     const int nch = (N + kBagChunk - 1) / kBagChunk;
     if (ix.vshift < 2 || ix.vshift > kWaveMaxVshift || ix.wstride <= 0 || (int64_t)nch * (1 << ix.vshift) > ix.cap ||
-        (int64_t)kBagSlot * ((T_ << ix.vshift) / kWaveParts + 1) > (int64_t)T_ * ix.cap)
+        (int64_t)kBagSlot * ((T_ << ix.vshift) / kWaveParts + 2) > (int64_t)T_ * ix.cap)
         return ctx_fail(ctx, DLRM_E_UNSUPPORTED, "bag build: N %d, vshift %d, capacity %lld", N, ix.vshift,
                         (long long)ix.cap);
     const PrepArgs pa{ix, tabs, T_, idx, itype, tstride, base, N, err};
