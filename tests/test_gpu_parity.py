@@ -455,6 +455,35 @@ def test_bag_wave_build_segments(pkg, gpu, rows, B, L, zipf, case):
         assert np.array_equal(to_np_f32(tabs[t].data), (-ref).astype(np.float32))
 
 
+@pytest.mark.parametrize("itype,base", [(torch.int64, 0), (torch.int32, 1)])
+def test_bag_build_int64_base_and_bounds(pkg, gpu, itype, base):
+    """The bag build (dlrm_indexer_build above 8192 positions per table) with int64 indices and with
+    1-based ones (the reference's): segments exactly numpy's; then one index past the end and one
+    below the base: the build leaves them out and raises the bounds flag, the prebuilt update writes
+    no row and raises BoundsError, as every dlrm_indexer_build does."""
+    rows, B, L, D = [3, 70000, 1_000_000], 1100, 9, 16
+    rng = np.random.default_rng(41)
+    idx = rand_indices(rng, rows, B, L, zipf=1.1)
+    tabs = pkg.EmbeddingTableSet([torch.zeros((n, D), device=gpu) for n in rows])
+    ix = pkg.SparseIndexer(len(rows), B * L, gpu)
+    p = pkg.PackedIndices(torch.from_numpy(idx + base).to(itype).to(gpu).reshape(len(rows), B, L))
+    ix.build(tabs, p, index_base=base)
+    tabs.ctx.check_bounds()
+    _assert_segments(ix, idx, B * L)
+    bad = idx + base
+    bad[1, 5000] = rows[1] + base
+    bad[2, 77] = base - 1
+    pb = pkg.PackedIndices(torch.from_numpy(bad).to(itype).to(gpu).reshape(len(rows), B, L))
+    ix.build(tabs, pb, index_base=base)
+    gi = torch.ones((B, len(rows) * D), device=gpu)
+    with pytest.raises(pkg.BoundsError):
+        pkg.update_(pkg.Descent(1.0), tabs, pkg.maplookup_pullback(0, tabs, pb, gi), ix, index_base=base,
+                    prebuilt=True)
+        tabs.ctx.check_bounds()
+    for t in tabs:
+        assert not t.data.any()  # no row written
+
+
 def test_indexer_footprint_compact(pkg, gpu):
     """the wave builds' per-part arrays are packed per table (round 6), so an indexer of
     26 tables x 16384 positions holds its 128-part build in a few hundred bytes per position
