@@ -70,13 +70,13 @@ def step_pipeline(w):
 
 
 def step_chunk(w):
-    """The wave build's chunk limit for workload `w` (HotPath(chunk=...), dlrm_indexer_set_chunk):
-    16 for uniform one-hot batches -- the 105-row Kaggle table's 17..32-position segments then run
-    as one-round hot-slice items: metric step 36.9 -> 36.4 us, 55.5 -> 56.1 M samples/s in an
-    alternating A/B, D = 16 unchanged (profiles/r14/chunk16_ab_*) -- and 32 for Zipf rows, whose
-    many more such segments turn into more hot-slice items than the apply launch has workgroups
-    (Terabyte bf16 52.5 -> 51.8 M with 16)."""
-    if w["lookups"] != 1 or w.get("zipf"):
+    """The wave build's chunk limit for workload `w` (HotPath(chunk=...), dlrm_indexer_set_chunk): 16
+    for one-hot batches -- the 105-row Kaggle table's 17..32-position segments then run as one-round
+    hot-slice items: metric step 36.9 -> 36.4 us, 55.5 -> 56.1 M samples/s in an alternating A/B, D = 16
+    unchanged at 16 parts and 85.6 vs 81.5 M at 32 (profiles/r14/chunk16_ab_*, profiles/r15/chunk_sweep)
+    -- and for Zipf rows too since they build 32 parts per table (step_parts): Terabyte bf16 58.1 / 58.5
+    vs 57.4 / 57.4 M (at 16 parts Zipf rows preferred 32: 52.5 vs 51.8 M, round 6 first session)."""
+    if w["lookups"] != 1 or (w.get("zipf") and not step_parts(w)):
         return None
     return 16
 
