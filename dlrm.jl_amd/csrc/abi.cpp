@@ -85,7 +85,7 @@ const Knobs& knobs() {
                          env_int("DLRM_BWD_SPLIT", 1) == 0,  env_int("DLRM_BWD_SPB", 0),
                          env_int("DLRM_BWD_CPL", 0),         env_int("DLRM_UPD_SBU", 1),
                          env_int("DLRM_WAVE_ROUNDS", 0),     env_int("DLRM_BAG_WAVE", 1) == 0,
-                         env_int("DLRM_BAG_VS", 0)};
+                         env_int("DLRM_BAG_VS", 0),          env_int("DLRM_BAG_SPLIT", 1)};
     return k;
 }
 int ctx_device(dlrm_ctx* ctx) { return ctx->device; }
@@ -807,6 +807,20 @@ int dlrm_indexer_build_split(dlrm_ctx* ctx, dlrm_indexer* ix, const dlrm_tables*
     CHECK_ARG(batch <= ix->dev.cap, "dlrm_indexer_build_split: batch %d > capacity %lld", batch,
               (long long)ix->dev.cap);
     ix->built = false;
+    // above the in-LDS build's 4096 positions: the bag build (configs[2]'s next-batch build at 8192, on
+    // a side stream beside the step: 94.5 vs 96.4 us per step with the in-LDS parts build -- its
+    // three launches are slower alone, 38.7 vs 17.7 us, but their small workgroups run beside the
+    // step's kernels, where the parts build's 104 workgroups of 136 KB LDS each held a whole CU;
+    // DESIGN.md §3 round 6).  DLRM_BAG_SPLIT=0: the parts / hash builds.
+    if (knobs().bag_split && batch > kFastMaxN && wave_fits(ix, batch)) {
+        ix->dev.vshift = wave_vshift(batch) - 1;
+        rc = launch_bag_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch,
+                              ctx_error_word(ctx));
+        if (rc) return rc;
+        record_build(ix, true, indices, itype, table_stride, index_base, batch, 1);
+        ix->dev.has_map = 1;
+        return DLRM_OK;
+    }
     ix->dev.vshift = build_vshift(ix, batch, true);
     rc = launch_indexer_build(ctx, ix->dev, tb->d_desc, tb->T, indices, itype, table_stride, index_base, batch, 1,
                               true, nullptr);

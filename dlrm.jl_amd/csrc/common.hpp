@@ -361,6 +361,8 @@ struct Knobs {
     int bag_hash;     // DLRM_BAG_WAVE=0: dlrm_indexer_build of 8192 < N <= 32768 positions per table (pooled
                       // bags) by the hash build instead of the bag build
     int bag_vs;       // DLRM_BAG_VS (2..8): the bag build's log2 parts per table (default wave_vshift(N))
+    int bag_split;    // DLRM_BAG_SPLIT=0: dlrm_indexer_build_split of 4096 < N <= 32768 by the in-LDS parts /
+                      // hash builds instead of the bag build
 };
 const Knobs& knobs();
 
