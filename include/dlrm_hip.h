@@ -220,7 +220,10 @@ int dlrm_indexer_create(dlrm_ctx* ctx, int num_tables, int64_t max_lookups_per_t
 int dlrm_indexer_destroy(dlrm_indexer* indexer);
 /* Dedupe: per table, group the lookup positions by row -> one segment per distinct row
  * holding the positions that hit it in ascending order (segment order is unspecified).
- * Asynchronous; device-side counts only. */
+ * Asynchronous; device-side counts only.  By batch * lookups positions per table: <= 4096 in LDS
+ * (one workgroup per table), <= 8192 in LDS over 4 parts, <= 32768 the bag build (count, place by
+ * part, per-part sort: pooled bags, round 6; DLRM_BAG_WAVE=0 selects the next form instead), above
+ * that the hash build.  Out-of-range indices are left out and raise the bounds flag. */
 int dlrm_indexer_build(dlrm_ctx* ctx, dlrm_indexer* indexer, const dlrm_tables* tables,
                        const void* indices, int itype, int64_t table_stride, int index_base,
                        int batch, int lookups);
